@@ -1,0 +1,510 @@
+"""Compile a parsed OpenSim model + env semantics + reference motion into a
+flat ModelPack (include/bioim_modelpack.h).
+
+What the compile does, in order:
+  1. topology: every OpenSim body is assigned to a *composite* body; a body
+     joined to its parent by a WeldJoint, or by a joint whose coordinates are
+     all locked, is merged into the parent's composite (rigidly attached);
+  2. functions: every TransformAxis / MovingPathPoint function becomes a
+     bioim_fn_t (SimmSpline coefficients fitted in :mod:`splines`);
+  3. forces: Millard muscles (curves from :mod:`curves`), Hunt-Crossley
+     spheres, CoordinateLimitForces (degree units folded in), and
+     CoordinateActuators;
+  4. env semantics and the reference tables.
+
+It also provides :func:`raw_forward_kinematics`, an FK computed straight from
+the parsed joints (no composites) — used to synthesize BodyKinematics
+reference tables and to cross-check the compiled topology in tests.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from . import packdef as P
+from .curves import muscle_curves
+from .osim import Function, Joint, OsimModel
+from .splines import simm_spline_coeffs
+
+DEG = math.pi / 180.0
+
+
+# ---------------------------------------------------------------- rotations
+def axis_rot(axis, angle):
+    a = np.asarray(axis, float)
+    n = np.linalg.norm(a)
+    if n == 0:
+        return np.eye(3)
+    a = a / n
+    x, y, z = a
+    c, s = math.cos(angle), math.sin(angle)
+    t = 1 - c
+    return np.array([[t * x * x + c, t * x * y - s * z, t * x * z + s * y],
+                     [t * x * y + s * z, t * y * y + c, t * y * z - s * x],
+                     [t * x * z - s * y, t * y * z + s * x, t * z * z + c]])
+
+
+def joint_transform(joint: Joint, qval: Dict[str, float]):
+    """X_FM(q) of a joint: body-fixed rotation sequence (rotation1..3) and
+    translations along F-frame axes (translation1..3)."""
+    R = np.eye(3)
+    p = np.zeros(3)
+    for k, ta in enumerate(joint.axes):
+        v = ta.func.value(qval.get(ta.coord, 0.0) if ta.coord else 0.0)
+        if k < 3:
+            R = R @ axis_rot(ta.axis, v)
+        else:
+            n = np.linalg.norm(ta.axis)
+            p = p + (ta.axis / n if n else ta.axis) * v
+    return R, p
+
+
+def compose(Xa, Xb):
+    Ra, pa = Xa
+    Rb, pb = Xb
+    return Ra @ Rb, Ra @ pb + pa
+
+
+def inverse(X):
+    R, p = X
+    return R.T, -R.T @ p
+
+
+def raw_forward_kinematics(model: OsimModel, qval: Dict[str, float]):
+    """Ground pose of every OpenSim body from the parsed joints; returns
+    ({body: (R, p)}, system COM)."""
+    poses = {'ground': (np.eye(3), np.zeros(3))}
+    pending = list(model.joints)
+    while pending:
+        rest = []
+        for j in pending:
+            if j.parent not in poses:
+                rest.append(j)
+                continue
+            qv = {c: (model.coords[c].default_value if model.coords[c].locked else qval.get(c, model.coords[c].default_value))
+                  for c in j.coords}
+            X_gf = compose(poses[j.parent], (j.R_pf, j.p_pf))
+            X_gm = compose(X_gf, joint_transform(j, qv))
+            poses[j.child] = compose(X_gm, inverse((j.R_cm, j.p_cm)))
+        if len(rest) == len(pending):
+            raise ValueError('disconnected joint tree')
+        pending = rest
+    msum = 0.0
+    com = np.zeros(3)
+    for name, b in model.bodies.items():
+        R, p = poses[name]
+        com += b.mass * (R @ b.com + p)
+        msum += b.mass
+    return poses, com / msum
+
+
+# ---------------------------------------------------------------- topology
+@dataclass
+class Topology:
+    cbody_joint: List[Joint]                 # inboard joint of each composite
+    cbody_parent: List[int]
+    body_cbody: Dict[str, int]
+    body_X: Dict[str, tuple]                 # X_comp_body
+    dof_of: Dict[str, int]
+
+
+def _is_rigid(model: OsimModel, j: Joint) -> bool:
+    if j.kind == 'WeldJoint':
+        return True
+    return all(model.coords[c].locked for c in j.coords)
+
+
+def build_topology(model: OsimModel) -> Topology:
+    by_child = {j.child: j for j in model.joints}
+    body_cbody: Dict[str, int] = {'ground': -1}
+    body_X: Dict[str, tuple] = {'ground': (np.eye(3), np.zeros(3))}
+    cbody_joint: List[Joint] = []
+    cbody_parent: List[int] = []
+    done = set(['ground'])
+    order = []
+    pending = list(model.body_order)
+    while pending:
+        rest = []
+        for b in pending:
+            j = by_child[b]
+            if j.parent not in done:
+                rest.append(b)
+                continue
+            order.append(b)
+            done.add(b)
+        if len(rest) == len(pending):
+            raise ValueError('joint tree not connected to ground')
+        pending = rest
+    for b in order:
+        j = by_child[b]
+        if _is_rigid(model, j) and j.parent != 'ground':
+            qv = {c: model.coords[c].default_value for c in j.coords}
+            X_pb = compose(compose((j.R_pf, j.p_pf), joint_transform(j, qv)), inverse((j.R_cm, j.p_cm)))
+            body_cbody[b] = body_cbody[j.parent]
+            body_X[b] = compose(body_X[j.parent], X_pb)
+        else:
+            body_cbody[b] = len(cbody_joint)
+            body_X[b] = (np.eye(3), np.zeros(3))
+            cbody_joint.append(j)
+            cbody_parent.append(body_cbody[j.parent])
+    dof_of = {}
+    for c in model.coord_order:
+        if not model.coords[c].locked and model.coords[c].joint in {j.name for j in cbody_joint}:
+            dof_of[c] = len(dof_of)
+    return Topology(cbody_joint, cbody_parent, body_cbody, body_X, dof_of)
+
+
+# ---------------------------------------------------------------- env specs
+@dataclass
+class EnvSpec:
+    env_id: str
+    muscle: bool
+    three_d: bool
+    cycle: int
+    n_episode: int
+    reset_hi: int
+    w_imitate: float = 0.8
+    w_effort: float = 0.2
+    w_action: float = 0.1
+    horizon: int = 5
+    use_target_obs: bool = True
+    use_grf: bool = True
+    max_actuation: float = 200.0
+    torso_y_min: float = 0.75
+    limit_force_max: float = 1000.0
+    acc_max: float = 1e4
+    action_r_scale: float = 1.0
+    reward_feet: bool = False
+    done_cross: bool = False
+    raw_action: bool = False
+    pd: bool = False
+    kp: Optional[List[float]] = None
+    kv: Optional[List[float]] = None
+    pd_coords: Optional[List[str]] = None
+    slow_twitch: Optional[List[float]] = None
+    nsub: int = 20
+    height: float = 1.80
+    test_mode: bool = False
+
+
+OBS_BPOS = ['torso', 'calcn_r', 'calcn_l', 'femur_r', 'femur_l', 'tibia_r', 'tibia_l', 'talus_r', 'talus_l',
+            'center_of_mass']
+OBS_BVEL = ['torso', 'calcn_r', 'calcn_l', 'center_of_mass']
+REF_BODIES = ['center_of_mass', 'femur_r', 'femur_l', 'tibia_r', 'tibia_l', 'talus_r', 'talus_l', 'calcn_r',
+              'calcn_l']
+
+
+def obs_dim_of(model: OsimModel, spec: EnvSpec) -> int:
+    nc = len(model.coord_order)
+    ntrans = sum(1 for c in ('pelvis_tx', 'pelvis_ty', 'pelvis_tz') if c in model.coords)
+    n = 1 + (nc - ntrans) + 2 * nc
+    if spec.use_target_obs:
+        n += 2 * (nc - 1)
+    n += 3 * len(OBS_BPOS) + 3 * len(OBS_BVEL)
+    if spec.muscle:
+        n += 3 * len(model.muscles)
+    if spec.use_grf:
+        n += 6 * len(model.hc_forces)
+    return n
+
+
+# ---------------------------------------------------------------- compile
+class _FnTable:
+    def __init__(self, pack):
+        self.pack = pack
+        self.n = 0
+        self.nk = 0
+
+    def add(self, f: Function, coord_index: int) -> int:
+        if self.n >= P.MAX_FN:
+            raise ValueError('too many functions')
+        e = self.pack.fn[self.n]
+        if f.kind == 'const':
+            e.type, e.coord, e.a, e.b = P.FN_CONST, -1, 0.0, f.b
+        elif f.kind == 'linear':
+            e.type, e.coord, e.a, e.b = P.FN_LINEAR, coord_index, f.a, f.b
+        else:
+            b, c, d = simm_spline_coeffs(f.x, f.y)
+            n = f.x.size
+            if self.nk + n > P.MAX_KNOTS:
+                raise ValueError('too many spline knots')
+            for i in range(n):
+                self.pack.knot_x[self.nk + i] = f.x[i]
+                self.pack.knot_y[self.nk + i] = f.y[i]
+                self.pack.knot_b[self.nk + i] = b[i]
+                self.pack.knot_c[self.nk + i] = c[i]
+                self.pack.knot_d[self.nk + i] = d[i]
+            e.type, e.coord, e.knot_off, e.nknots, e.a, e.b = P.FN_SPLINE, coord_index, self.nk, n, f.a, 0.0
+            self.nk += n
+        self.n += 1
+        return self.n - 1
+
+
+def _set_vec(dst, v):
+    for i, x in enumerate(np.asarray(v, float).reshape(-1)):
+        dst[i] = float(x)
+
+
+def _set_curve(dst, curve):
+    dst.nseg = curve.nseg
+    for s in range(curve.nseg):
+        for k in range(6):
+            dst.x[s][k] = float(curve.x[s, k])
+            dst.y[s][k] = float(curve.y[s, k])
+    dst.x0, dst.y0, dst.dydx0 = float(curve.x0), float(curve.y0), float(curve.dydx0)
+    dst.x1, dst.y1, dst.dydx1 = float(curve.x1), float(curve.y1), float(curve.dydx1)
+
+
+def compile_pack(model: OsimModel, spec: EnvSpec, ref: dict) -> P.ModelPack:
+    """``ref``: dict(time (R,), q (R, ncoord), u (R, ncoord), x (R, 9, 3)) in
+    CoordinateSet order / REF_BODIES order, already resampled at 0.01 s."""
+    pk = P.ModelPack()
+    pk.magic, pk.version = P.MAGIC, P.VERSION
+    pk.env_id = spec.env_id.encode()[:47]
+    topo = build_topology(model)
+    cidx = {c: i for i, c in enumerate(model.coord_order)}
+    if len(model.coord_order) > P.MAX_COORD or len(topo.cbody_joint) > P.MAX_CBODY:
+        raise ValueError('model too large for the pack')
+
+    # coordinates
+    pk.ncoord = len(model.coord_order)
+    pk.ndof = len(topo.dof_of)
+    jname_cb = {j.name: i for i, j in enumerate(topo.cbody_joint)}
+    for i, cn in enumerate(model.coord_order):
+        c = model.coords[cn]
+        e = pk.coord[i]
+        e.motion = 0 if c.motion == 'rotational' else 1
+        e.locked = 1 if cn not in topo.dof_of else 0
+        e.dof = topo.dof_of.get(cn, -1)
+        e.cbody = jname_cb.get(c.joint, -1)
+        e.default_value, e.range_min, e.range_max = c.default_value, c.range[0], c.range[1]
+
+    fns = _FnTable(pk)
+
+    # composite bodies
+    pk.ncbody = len(topo.cbody_joint)
+    members: Dict[int, List[str]] = {}
+    for b in model.body_order:
+        members.setdefault(topo.body_cbody[b], []).append(b)
+    for ci, j in enumerate(topo.cbody_joint):
+        e = pk.cbody[ci]
+        e.parent = topo.cbody_parent[ci]
+        X_pc_pb = topo.body_X[j.parent]
+        R_pf, p_pf = compose(X_pc_pb, (j.R_pf, j.p_pf))
+        R_mb, p_mb = inverse((j.R_cm, j.p_cm))
+        _set_vec(e.R_pf, R_pf)
+        _set_vec(e.p_pf, p_pf)
+        _set_vec(e.R_mb, R_mb)
+        _set_vec(e.p_mb, p_mb)
+        for k, ta in enumerate(j.axes):
+            n = np.linalg.norm(ta.axis)
+            _set_vec(e.axis[k], ta.axis / n if n else ta.axis)
+            if ta.func.kind == 'const' and ta.func.b == 0.0:
+                e.fn[k] = -1
+            else:
+                e.fn[k] = fns.add(ta.func, cidx[ta.coord] if ta.coord else -1)
+        # merged mass properties
+        mtot = 0.0
+        cm = np.zeros(3)
+        for b in members[ci]:
+            R, p = topo.body_X[b]
+            mb = model.bodies[b]
+            mtot += mb.mass
+            cm += mb.mass * (R @ mb.com + p)
+        cm = cm / mtot if mtot > 0 else cm
+        I = np.zeros((3, 3))
+        for b in members[ci]:
+            R, p = topo.body_X[b]
+            mb = model.bodies[b]
+            xx, yy, zz, xy, xz, yz = mb.inertia
+            Ib = np.array([[xx, xy, xz], [xy, yy, yz], [xz, yz, zz]])
+            d = R @ mb.com + p - cm
+            I += R @ Ib @ R.T + mb.mass * (d @ d * np.eye(3) - np.outer(d, d))
+        e.mass = mtot
+        _set_vec(e.com, cm)
+        _set_vec(e.inertia, [I[0, 0], I[1, 1], I[2, 2], I[0, 1], I[0, 2], I[1, 2]])
+
+    # OpenSim bodies
+    pk.nosbody = len(model.body_order)
+    bidx = {b: i for i, b in enumerate(model.body_order)}
+    for i, b in enumerate(model.body_order):
+        e = pk.osbody[i]
+        e.cbody = topo.body_cbody[b]
+        R, p = topo.body_X[b]
+        _set_vec(e.R, R)
+        _set_vec(e.p, p)
+        e.mass = model.bodies[b].mass
+        _set_vec(e.com, model.bodies[b].com)
+
+    # muscles
+    pk.nmuscle = len(model.muscles) if spec.muscle else 0
+    npt = 0
+    if spec.muscle:
+        st = spec.slow_twitch or [0.5] * len(model.muscles)
+        for mi, mu in enumerate(model.muscles):
+            e = pk.muscle[mi]
+            e.pt_off = npt
+            for pt in mu.path:
+                pe = pk.pathpt[npt]
+                cb = topo.body_cbody[pt.body]
+                R, p = topo.body_X[pt.body]
+                pe.cbody = cb
+                if pt.kind == 'moving':
+                    pe.type = P.PT_MOVING
+                    _set_vec(pe.loc, pt.loc)
+                    _set_vec(pe.R, R)
+                    _set_vec(pe.p, p)
+                    for k in range(3):
+                        f = pt.move[k]
+                        pe.fn[k] = -1 if f is None else fns.add(f, cidx[f.coord] if f.coord else -1)
+                else:
+                    _set_vec(pe.loc, R @ pt.loc + p)
+                    pe.fn[0] = pe.fn[1] = pe.fn[2] = -1
+                    if pt.kind == 'cond':
+                        pe.type = P.PT_COND
+                        pe.cond_coord = cidx[pt.cond_coord]
+                        pe.range_lo, pe.range_hi = pt.cond_range
+                    else:
+                        pe.type = P.PT_FIXED
+                npt += 1
+            e.npt = npt - e.pt_off
+            e.fiso, e.lopt, e.lts, e.alpha_opt, e.vmax = mu.fiso, mu.lopt, mu.lts, mu.alpha_opt, mu.vmax
+            e.tau_act, e.tau_deact = mu.tau_act, mu.tau_deact
+            e.amin = float(mu.props.get('minimum_activation', 0.01))
+            e.damping = float(mu.props.get('fiber_damping', 0.1))
+            e.default_act = float(mu.props.get('default_activation', 0.05))
+            e.width = mu.lopt * math.sin(mu.alpha_opt)
+            fal, fv, fpe, fse = muscle_curves(mu.curves)
+            max_pen = math.acos(0.1)
+            e.lmin = max(1e-8, max(fal.x0 * mu.lopt, e.width / math.sin(max_pen)))
+            e.slow_twitch = st[mi]
+            e.mass = mu.fiso / 0.25e6 * 1059.7 * mu.lopt
+            _set_curve(e.fal, fal)
+            _set_curve(e.fv, fv)
+            _set_curve(e.fpe, fpe)
+            _set_curve(e.fse, fse)
+    pk.npathpt = npt
+
+    # contact
+    sph_names = {}
+    for hs in model.halfspaces:
+        if hs.body != 'ground' or np.any(np.abs(hs.loc) > 0) or abs(hs.orientation[2] + math.pi / 2) > 1e-12 \
+                or abs(hs.orientation[0]) > 0 or abs(hs.orientation[1]) > 0:
+            raise NotImplementedError('only the ground plane y=0 half space is supported')
+    ns = 0
+    for fi, hc in enumerate(model.hc_forces):
+        ce = pk.cforce[fi]
+        ce.stiffness, ce.dissipation = hc.stiffness, hc.dissipation
+        ce.static_friction, ce.dynamic_friction = hc.static_friction, hc.dynamic_friction
+        ce.viscous_friction, ce.transition_velocity = hc.viscous_friction, hc.transition_velocity
+        for g in hc.geometries:
+            if g in [h.name for h in model.halfspaces]:
+                continue
+            sp = next(s for s in model.spheres if s.name == g)
+            se = pk.sphere[ns]
+            se.cbody = topo.body_cbody[sp.body]
+            se.force = fi
+            R, p = topo.body_X[sp.body]
+            _set_vec(se.loc, R @ sp.loc + p)
+            se.radius = sp.radius
+            sph_names[g] = ns
+            ns += 1
+    pk.nsphere = ns
+    pk.ncforce = len(model.hc_forces)
+
+    # coordinate limit forces
+    pk.nlimit = len(model.limits)
+    for li, lf in enumerate(model.limits):
+        e = pk.limit[li]
+        c = model.coords[lf.coord]
+        e.coord = cidx[lf.coord]
+        e.dof = topo.dof_of.get(lf.coord, -1)
+        if c.motion == 'rotational':
+            w, s = 180.0 / math.pi, DEG
+        else:
+            w, s = 1.0, 1.0
+        e.qup, e.qlow, e.trans = lf.upper_limit * s, lf.lower_limit * s, lf.transition * s
+        e.kup, e.klow, e.damping = lf.upper_stiffness * w, lf.lower_stiffness * w, lf.damping * w
+
+    # coordinate actuators
+    pk.ncoordact = len(model.coord_actuators) if not spec.muscle else 0
+    if not spec.muscle:
+        for ai, ca in enumerate(model.coord_actuators):
+            e = pk.coordact[ai]
+            e.coord = cidx[ca.coord]
+            e.dof = topo.dof_of.get(ca.coord, -1)
+            e.optimal_force, e.min_control, e.max_control = ca.optimal_force, ca.min_control, ca.max_control
+    pk.nfn, pk.nknots = fns.n, fns.nk
+
+    # env semantics
+    flags = 0
+    flags |= P.ENV_MUSCLE if spec.muscle else 0
+    flags |= P.ENV_HAS_TZ if 'pelvis_tz' in model.coords else 0
+    flags |= P.ENV_REWARD_FEET if spec.reward_feet else 0
+    flags |= P.ENV_DONE_CROSS if spec.done_cross else 0
+    flags |= P.ENV_RAW_ACTION if spec.raw_action else 0
+    flags |= P.ENV_TARGET_OBS if spec.use_target_obs else 0
+    flags |= P.ENV_GRF_OBS if spec.use_grf else 0
+    flags |= P.ENV_PD if spec.pd else 0
+    pk.env_flags = flags
+    pk.nact = pk.nmuscle if spec.muscle else (len(spec.kp) if spec.pd else pk.ncoordact)
+    pk.obs_dim = obs_dim_of(model, spec)
+    pk.info_dim = 5 if spec.muscle else 4
+    pk.nsub, pk.horizon, pk.cycle = spec.nsub, spec.horizon, spec.cycle
+    pk.n_episode, pk.reset_hi = spec.n_episode, spec.reset_hi
+    pk.coord_tx = cidx.get('pelvis_tx', -1)
+    pk.coord_ty = cidx.get('pelvis_ty', -1)
+    pk.coord_tz = cidx.get('pelvis_tz', -1)
+    pk.torso_body, pk.calcn_r_body, pk.calcn_l_body = bidx['torso'], bidx['calcn_r'], bidx['calcn_l']
+    pk.n_obs_bpos, pk.n_obs_bvel = len(OBS_BPOS), len(OBS_BVEL)
+    for i, b in enumerate(OBS_BPOS):
+        pk.obs_bpos[i] = bidx.get(b, -1)
+    for i, b in enumerate(OBS_BVEL):
+        pk.obs_bvel[i] = bidx.get(b, -1)
+    for i, b in enumerate(REF_BODIES):
+        pk.rw_body[i] = bidx.get(b, -1)
+    if spec.pd:
+        for i, cn in enumerate(spec.pd_coords):
+            pk.pd_coord[i] = cidx[cn]
+            pk.kp[i], pk.kv[i] = spec.kp[i], spec.kv[i]
+    pk.step_size = 0.01
+    pk.w_imitate, pk.w_effort, pk.w_action = spec.w_imitate, spec.w_effort, spec.w_action
+    pk.action_r_scale, pk.max_actuation = spec.action_r_scale, spec.max_actuation
+    pk.total_mass = model.total_mass()
+    _set_vec(pk.gravity, model.gravity)
+    pk.height = spec.height
+    pk.torso_y_min, pk.limit_force_max, pk.acc_max = spec.torso_y_min, spec.limit_force_max, spec.acc_max
+
+    # reference motion
+    nrows = ref['time'].shape[0]
+    if nrows > P.MAX_REFROWS:
+        raise ValueError('reference motion too long')
+    pk.nrows = nrows
+    for r in range(nrows):
+        t = float(ref['time'][r])
+        pk.ref_time[r] = t
+        pk.ref_istep[r] = int(t / 0.01)  # opensim_wrapper.py:306 float64 truncation
+        for c in range(pk.ncoord):
+            pk.ref_q[r][c] = float(ref['q'][r, c])
+            pk.ref_u[r][c] = float(ref['u'][r, c])
+        for k in range(P.NREFBODY):
+            for a in range(3):
+                pk.ref_x[r][k][a] = float(ref['x'][r, k, a])
+    return pk
+
+
+def pack_bytes(pk: P.ModelPack) -> bytes:
+    return ctypes.string_at(ctypes.addressof(pk), ctypes.sizeof(pk))
+
+
+def pack_from_bytes(b: bytes) -> P.ModelPack:
+    if len(b) != ctypes.sizeof(P.ModelPack):
+        raise ValueError(f'pack size {len(b)} != {ctypes.sizeof(P.ModelPack)}')
+    pk = P.ModelPack.from_buffer_copy(b)
+    if pk.magic != P.MAGIC or pk.version != P.VERSION:
+        raise ValueError('bad ModelPack magic/version')
+    return pk

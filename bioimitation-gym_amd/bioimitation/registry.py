@@ -1,0 +1,103 @@
+"""Registered environment IDs and their compile recipes.
+
+Mirrors ``bioimitation/__init__.py:23-143`` (gym ``register`` + Ray
+``register_env``): every ID maps to (model source, load-time transforms, env
+semantics).  The env semantics are read off each reference env class, cited
+per entry.  Compiled packs live in ``bioimitation/data/packs/<ID>.npz``.
+"""
+from __future__ import annotations
+
+from .modelpack import EnvSpec
+
+SLOW_TWITCH_2D = [0.499, 0.55, 0.5, 0.484, 0.546, 0.759, 0.721, 0.499, 0.55, 0.5, 0.484, 0.546, 0.759, 0.721]
+SLOW_TWITCH_3D = [0.499, 0.55, 0.5, 0.484, 0.546, 0.759, 0.721, 0.484, 0.546, 0.759, 0.721, 0.499, 0.55, 0.5,
+                  0.484, 0.546, 0.759, 0.721, 0.484, 0.546, 0.759, 0.721]
+
+PD_COORDS_2D = ['pelvis_tilt', 'hip_flexion_r', 'knee_angle_r', 'ankle_angle_r',
+                'hip_flexion_l', 'knee_angle_l', 'ankle_angle_l']
+
+# env id -> (model file relative to the reference data dir, transforms, spec kwargs)
+RECIPES = {
+    # torque_walking_imitation_env2D.py:18-366 (PD :117-149, done :249-277, reward :279-366)
+    'TorqueWalkingImitation2D-v0': dict(
+        model='2D/scale/model_scaled.osim', transforms=('predictive', 'torque'),
+        reference='2D/walking_reference_data',
+        spec=dict(muscle=False, three_d=False, cycle=132, n_episode=264, reset_hi=132,
+                  acc_max=1e5, pd=True, pd_coords=PD_COORDS_2D,
+                  kp=[100, 100, 100, 50, 100, 100, 50], kv=[5, 5, 5, 2, 5, 5, 2])),
+    # muscle_walking_imitation_env2D.py:17-403 (done :237-265, reward :267-358, COT :360-403)
+    'MuscleWalkingImitation2D-v0': dict(
+        model='2D/scale/model_scaled.osim', transforms=('predictive',),
+        reference='2D/walking_reference_data',
+        spec=dict(muscle=True, three_d=False, cycle=132, n_episode=264, reset_hi=132,
+                  acc_max=1e4, slow_twitch=SLOW_TWITCH_2D)),
+}
+
+REGISTERED_IDS = [
+    'TorqueWalkingImitation2D-v0', 'TorqueRunningImitation2D-v0', 'TorqueJumpingImitation2D-v0',
+    'TorqueLockedKneeImitation2D-v0', 'TorqueWalkingImitation3D-v0', 'TorqueRunningImitation3D-v0',
+    'TorqueJumpingImitation3D-v0', 'TorqueLockedKneeImitation3D-v0',
+    'MuscleWalkingImitation2D-v0', 'MuscleRunningImitation2D-v0', 'MuscleJumpingImitation2D-v0',
+    'MuscleLockedKneeImitation2D-v0', 'MuscleWalkingImitation3D-v0', 'MuscleRunningImitation3D-v0',
+    'MuscleJumpingImitation3D-v0', 'MuscleLockedKneeImitation3D-v0', 'MusclePalsyImitation3D-v0',
+]
+
+
+def env_spec(env_id: str, config: dict = None) -> EnvSpec:
+    """EnvSpec for an ID with the user's env config (configs/env_default.py:7-15)."""
+    cfg = dict(config or {})
+    r = RECIPES[env_id]
+    kw = dict(r['spec'])
+    if 'r_weights' in cfg:
+        kw['w_imitate'], kw['w_effort'], kw['w_action'] = [float(v) for v in cfg['r_weights']]
+    if 'horizon' in cfg:
+        kw['horizon'] = int(cfg['horizon'])
+    if 'use_target_obs' in cfg:
+        kw['use_target_obs'] = bool(cfg['use_target_obs'])
+    if 'use_GRF' in cfg:
+        kw['use_grf'] = bool(cfg['use_GRF'])
+    if 'max_actuation' in cfg:
+        kw['max_actuation'] = float(cfg['max_actuation'])
+    return EnvSpec(env_id=env_id, **kw)
+
+
+def _pack_path(env_id: str) -> str:
+    import os
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), 'data', 'packs', env_id + '.npz')
+
+
+def load_pack(env_id: str, config: dict = None):
+    """The committed ModelPack of ``env_id`` with the user's env config
+    applied (reward weights, horizon, obs switches, test mode)."""
+    import numpy as np
+    from . import packdef as P
+    from .modelpack import pack_from_bytes
+    if env_id not in RECIPES:
+        if env_id in REGISTERED_IDS:
+            raise NotImplementedError(f'{env_id} is registered by the reference but not built yet')
+        raise KeyError(env_id)
+    with np.load(_pack_path(env_id), allow_pickle=False) as z:
+        pk = pack_from_bytes(z['pack'].tobytes())
+    cfg = dict(config or {})
+    spec = env_spec(env_id, cfg)
+    pk.w_imitate, pk.w_effort, pk.w_action = spec.w_imitate, spec.w_effort, spec.w_action
+    if spec.horizon < 1 or spec.horizon > P.MAX_HORIZON:
+        raise ValueError(f'horizon must be in [1, {P.MAX_HORIZON}]')
+    pk.horizon = spec.horizon
+    pk.max_actuation = spec.max_actuation
+    flags = pk.env_flags & ~(P.ENV_TARGET_OBS | P.ENV_GRF_OBS)
+    flags |= P.ENV_TARGET_OBS if spec.use_target_obs else 0
+    flags |= P.ENV_GRF_OBS if spec.use_grf else 0
+    pk.env_flags = flags
+    ntrans = sum(1 for c in (pk.coord_tx, pk.coord_ty, pk.coord_tz) if c >= 0)
+    n = 1 + (pk.ncoord - ntrans) + 2 * pk.ncoord
+    n += 2 * (pk.ncoord - 1) if spec.use_target_obs else 0
+    n += 3 * pk.n_obs_bpos + 3 * pk.n_obs_bvel + 3 * pk.nmuscle
+    n += 6 * pk.ncforce if spec.use_grf else 0
+    pk.obs_dim = n
+    if cfg.get('mode') == 'test':
+        pk.n_episode = pk.nrows - 2   # muscle_walking_imitation_env2D.py:74-75
+        pk.reset_hi = 0               # reset index 0 in test mode (:141-142)
+    if 'nsub' in cfg:
+        pk.nsub = int(cfg['nsub'])
+    return pk

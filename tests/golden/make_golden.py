@@ -1,0 +1,450 @@
+"""Generate env-level golden vectors from the reference's OWN env classes.
+
+Runs in the dev container only (needs /root/reference); the committed outputs
+(tests/golden/*.npz) are what the tests read.
+
+How: the reference env modules (e.g. ``muscle_walking_imitation_env2D.py``) are
+imported from /root/reference with their third-party imports stubbed
+(``opensim``, ``gym``, ``flatten_dict`` — absent here) and their package
+``__init__`` files bypassed.  ``OsimEnv`` builds an ``OsimModel``
+(``opensim_environment.py:37``); we substitute ``FakeOsimModel``, a
+restatement of the ``opensim_wrapper.py`` facade whose physics is the fp64 C
+oracle's ``orc_osim_*`` boundary.  The reference's own code then performs
+action smoothing, the PD law, actuation order, observation assembly
+(``flatten``), reward, cost of transport, termination and reset.  Each
+episode records (reset index, actions, obs, reward, done, info); the oracle's
+fused ``orc_env_step`` must reproduce them (tests/test_golden.py), which pins
+the env semantics.  The physics itself is not pinned (OpenSim unavailable).
+
+    python tests/golden/make_golden.py
+"""
+import importlib
+import importlib.util
+import math
+import os
+import random
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = '/root/reference'
+PKG = os.path.join(REPO, 'bioimitation-gym_amd', 'bioimitation')
+
+
+def _load_by_path(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+# our own modules, loaded under an alias (the reference also owns the name 'bioimitation')
+amd = types.ModuleType('bioim_amd')
+amd.__path__ = [PKG]
+sys.modules['bioim_amd'] = amd
+P = _load_by_path('bioim_amd.packdef', os.path.join(PKG, 'packdef.py'))
+_load_by_path('bioim_amd.splines', os.path.join(PKG, 'splines.py'))
+_load_by_path('bioim_amd.osim', os.path.join(PKG, 'osim.py'))
+_load_by_path('bioim_amd.curves', os.path.join(PKG, 'curves.py'))
+_load_by_path('bioim_amd.modelpack', os.path.join(PKG, 'modelpack.py'))
+registry = _load_by_path('bioim_amd.registry', os.path.join(PKG, 'registry.py'))
+storage = _load_by_path('bioim_amd.storage', os.path.join(PKG, 'storage.py'))
+sys.path.insert(0, os.path.join(REPO, 'oracle'))
+import oracle as oracle_mod  # noqa: E402
+import ctypes as C  # noqa: E402
+
+# ------------------------------------------------------------------ stubs
+opensim = types.ModuleType('opensim')
+sys.modules['opensim'] = opensim
+gym = types.ModuleType('gym')
+
+
+class _Env:
+    pass
+
+
+class _Box:
+    def __init__(self, low, high):
+        self.low, self.high = np.asarray(low), np.asarray(high)
+
+
+gym.Env = _Env
+gym.spaces = types.ModuleType('gym.spaces')
+gym.spaces.Box = _Box
+sys.modules['gym'] = gym
+sys.modules['gym.spaces'] = gym.spaces
+fd = types.ModuleType('flatten_dict')
+
+
+def _flatten(d, parent=()):
+    """flatten_dict.flatten (tuple reducer): nested dicts -> {key tuple: leaf}."""
+    out = {}
+    for k, v in d.items():
+        if isinstance(v, dict) and v:
+            out.update(_flatten(v, parent + (k,)))
+        else:
+            out[parent + (k,)] = v
+    return out
+
+
+fd.flatten = lambda d: _flatten(d)
+sys.modules['flatten_dict'] = fd
+
+# reference package skeleton without running its __init__ files
+for name, rel in [('bioimitation', 'bioimitation'), ('bioimitation.imitation_envs', 'bioimitation/imitation_envs'),
+                  ('bioimitation.imitation_envs.utils', 'bioimitation/imitation_envs/utils'),
+                  ('bioimitation.imitation_envs.envs', 'bioimitation/imitation_envs/envs'),
+                  ('bioimitation.imitation_envs.envs.muscle', 'bioimitation/imitation_envs/envs/muscle'),
+                  ('bioimitation.imitation_envs.envs.muscle.planar', 'bioimitation/imitation_envs/envs/muscle/planar'),
+                  ('bioimitation.imitation_envs.envs.torque', 'bioimitation/imitation_envs/envs/torque'),
+                  ('bioimitation.imitation_envs.envs.torque.planar', 'bioimitation/imitation_envs/envs/torque/planar')]:
+    m = types.ModuleType(name)
+    m.__path__ = [os.path.join(REF, rel)]
+    sys.modules[name] = m
+
+oenv = importlib.import_module('bioimitation.imitation_envs.utils.opensim_environment')
+
+# ------------------------------------------------------------------ fake facade
+CURRENT = {}
+
+
+class _Set:
+    def __init__(self, items):
+        self.items = items
+
+    def getSize(self):
+        return len(self.items)
+
+    def get(self, i):
+        return self.items[i]
+
+
+class _Muscle:
+    def __init__(self, fm, i):
+        self.fm, self.i = fm, i
+
+    def getName(self):
+        return self.fm.muscle_names[self.i]
+
+    def getMaxIsometricForce(self):
+        return self.fm.pack.muscle[self.i].fiso
+
+    def getOptimalFiberLength(self):
+        return self.fm.pack.muscle[self.i].lopt
+
+    def _r(self, k):
+        return self.fm.muscle_report()[self.i][k]
+
+    def getActivation(self, s):
+        return self._r(0)
+
+    def getFiberLength(self, s):
+        return self._r(1)
+
+    def getFiberVelocity(self, s):
+        return self._r(2)
+
+    def getFiberForce(self, s):
+        return self._r(3)
+
+    def getActiveFiberForce(self, s):
+        return self._r(4)
+
+    def getExcitation(self, s):
+        return self._r(5)
+
+
+class _Model:
+    def __init__(self, fm):
+        self.fm = fm
+
+    def getTotalMass(self, state):
+        return self.fm.pack.total_mass
+
+    def getGravity(self):
+        return [self.fm.pack.gravity[i] for i in range(3)]
+
+    def getMuscles(self):
+        return _Set([_Muscle(self.fm, i) for i in range(self.fm.pack.nmuscle)])
+
+
+class FakeOsimModel:
+    """opensim_wrapper.OsimModel restated over the oracle's orc_osim_* boundary."""
+
+    def __init__(self, model_path, step_size, integrator_accuracy, visualize):
+        self.pack = CURRENT['pack']
+        self.orc = CURRENT['oracle']
+        self.names = CURRENT['names']
+        self.envbuf = self.orc.new_envs(1)
+        self.e = self.orc.env_ptr(self.envbuf, 0)
+        self.step_size = step_size
+        self.istep = 0
+        self.state = None
+        self.model = _Model(self)
+        pk = self.pack
+        self.coordinate_names = list(self.names['coords'])
+        self.muscle_names = list(self.names['muscles'])
+        self.is_muscle_model = pk.nmuscle > 0
+        if pk.nmuscle:
+            self.action_min, self.action_max = [0.0] * pk.nmuscle, [1.0] * pk.nmuscle
+        else:
+            self.action_min = [pk.coordact[i].min_control for i in range(pk.ncoordact)]
+            self.action_max = [pk.coordact[i].max_control for i in range(pk.ncoordact)]
+        self._rep = None
+        CURRENT['fake'] = self
+
+    # state mutation ----------------------------------------------------
+    def _dirty(self):
+        self._rep = None
+
+    def reset(self):
+        self.orc.lib.orc_osim_reset(self.orc.pk, self.e)
+        self.istep = 0
+        self._dirty()
+
+    def set_time(self, t):
+        self.orc.lib.orc_osim_set_time(self.orc.pk, self.e, C.c_double(float(t)))
+        self.istep = int(float(t) / self.step_size)
+        CURRENT['reset_time'] = float(t)
+        self._dirty()
+
+    def _set(self, d, speeds):
+        v = np.zeros(self.pack.ncoord)
+        have = np.zeros(self.pack.ncoord, bool)
+        for name, val in d.items():
+            i = self.coordinate_names.index(name)
+            v[i], have[i] = float(val), True
+        cur = self.report()
+        base = cur['u'] if speeds else cur['q']
+        v[~have] = base[~have]
+        self.orc.lib.orc_osim_set_coords(self.orc.pk, self.e, v.ctypes.data_as(C.POINTER(C.c_double)), int(speeds))
+        self._dirty()
+
+    def set_coordinates(self, q_dict):
+        self._set(q_dict, False)
+
+    def set_velocities(self, u_dict):
+        self._set(u_dict, True)
+
+    def actuate(self, action):
+        if np.any(np.isnan(action)):
+            action = np.zeros(action.shape)
+        action = np.clip(np.array(action), self.action_min, self.action_max)
+        self.last_action = action
+        a = np.ascontiguousarray(action, dtype=np.float64)
+        self.orc.lib.orc_osim_actuate(self.orc.pk, self.e, a.ctypes.data_as(C.POINTER(C.c_double)))
+        self._dirty()
+
+    def integrate(self):
+        self.istep += 1
+        self.orc.lib.orc_osim_integrate(self.orc.pk, self.e)
+        self._dirty()
+
+    # realized state ----------------------------------------------------
+    def report(self):
+        if self._rep is None:
+            pk = self.pack
+            n = self.orc.lib.orc_osim_report_dim(self.orc.pk)
+            out = np.zeros(n)
+            self.orc.lib.orc_osim_report(self.orc.pk, self.e, out.ctypes.data_as(C.POINTER(C.c_double)))
+            nc, nb, nm, nf, nl = pk.ncoord, pk.nosbody, pk.nmuscle, pk.ncforce, pk.nlimit
+            k = 0
+            r = {}
+            r['q'], k = out[k:k + nc], k + nc
+            r['u'], k = out[k:k + nc], k + nc
+            r['qdd'], k = out[k:k + nc], k + nc
+            r['bodies'], k = out[k:k + 6 * (nb + 1)].reshape(nb + 1, 6), k + 6 * (nb + 1)
+            r['muscles'], k = out[k:k + 6 * nm].reshape(nm, 6), k + 6 * nm
+            r['contact'], k = out[k:k + 6 * nf].reshape(nf, 6), k + 6 * nf
+            r['limits'], k = out[k:k + nl], k + nl
+            r['time'] = out[k]
+            self._rep = r
+        return self._rep
+
+    def muscle_report(self):
+        return self.report()['muscles']
+
+    def calc_joint_kinematics(self):
+        r = self.report()
+        obs = {'time': r['time'], 'coordinate_pos': {}, 'coordinate_vel': {}, 'coordinate_acc': {}}
+        for i, n in enumerate(self.coordinate_names):
+            obs['coordinate_pos'][n] = float(r['q'][i])
+            obs['coordinate_vel'][n] = float(r['u'][i])
+            obs['coordinate_acc'][n] = float(r['qdd'][i])
+        return obs
+
+    def calc_body_kinematics(self):
+        r = self.report()
+        obs = {'time': r['time']}
+        for k in ('body_pos', 'body_vel', 'body_acc', 'body_pos_rot', 'body_vel_rot', 'body_acc_rot'):
+            obs[k] = {}
+        for i, n in enumerate(self.names['bodies']):
+            obs['body_pos'][n] = [float(x) for x in r['bodies'][i, :3]]
+            obs['body_vel'][n] = [float(x) for x in r['bodies'][i, 3:]]
+            for k in ('body_acc', 'body_pos_rot', 'body_vel_rot', 'body_acc_rot'):
+                obs[k][n] = [0.0, 0.0, 0.0]
+        obs['body_pos']['center_of_mass'] = [float(x) for x in r['bodies'][-1, :3]]
+        obs['body_vel']['center_of_mass'] = [float(x) for x in r['bodies'][-1, 3:]]
+        obs['body_acc']['center_of_mass'] = [0.0, 0.0, 0.0]
+        return obs
+
+    def calc_forces_info(self):
+        r = self.report()
+        obs = {'time': r['time'], 'forces': {}, 'contact_forces': {}, 'coordinate_limit_forces': {},
+               'scalar_actuator_forces': {}}
+        for i, n in enumerate(self.names['cforces']):
+            ground = [-float(x) for x in r['contact'][i]]        # getRecordValues: wrench on the platform
+            obs['contact_forces'][n] = [-g for g in ground]      # opensim_wrapper.py:211-219 negates
+        for i, n in enumerate(self.names['limits']):
+            obs['coordinate_limit_forces'][n] = float(r['limits'][i])
+        return obs
+
+    def calc_muscles_info(self):
+        r = self.report()
+        obs = {'time': r['time']}
+        if self.pack.nmuscle:
+            obs['muscles'] = {}
+            for i, n in enumerate(self.muscle_names):
+                m = r['muscles'][i]
+                obs['muscles'][n] = {'activation': float(m[0]), 'fiber_length': float(m[1]),
+                                     'fiber_velocity': float(m[2]), 'fiber_force': float(m[3])}
+        return obs
+
+    def get_action_space_size(self):
+        return len(self.action_min)
+
+
+oenv.OsimModel = FakeOsimModel
+
+
+def _names(env_id):
+    sys.path.insert(0, os.path.join(REPO, 'bioimitation-gym_amd', 'tools'))
+    osim = sys.modules['bioim_amd.osim']
+    tr = _load_by_path('bioim_amd.transforms', os.path.join(PKG, 'transforms.py'))
+    rec = registry.RECIPES[env_id]
+    m = osim.load_osim(os.path.join(REF, 'bioimitation/imitation_envs/data', rec['model']))
+    for t in rec['transforms']:
+        m = tr.construct_predictive_model(m) if t == 'predictive' else \
+            tr.convert_model_to_torque_actuated(m, 200.0) if t == 'torque' else tr.convert_model_to_prosthetic(m)
+    return dict(coords=list(m.coord_order), bodies=list(m.body_order),
+                muscles=[mu.name for mu in m.muscles] if registry.RECIPES[env_id]['spec']['muscle'] else [],
+                cforces=[h.name for h in m.hc_forces], limits=[l.name for l in m.limits])
+
+
+def make_env(env_id, modname, clsname, config):
+    pk = registry.load_pack(env_id, config)
+    CURRENT['pack'] = pk
+    CURRENT['oracle'] = oracle_mod.Oracle(pk)
+    CURRENT['names'] = _names(env_id)
+    mod = importlib.import_module(modname)
+    ref_dir = os.path.join(PKG, 'data', registry.RECIPES[env_id]['reference'])
+
+    def fake_read(model_file, file_name, step):
+        return storage.read_from_storage(os.path.join(ref_dir, os.path.basename(file_name)), step)
+    mod.read_from_storage = fake_read
+    mod.construct_predictive_model = lambda *a, **k: None
+    if hasattr(mod, 'convert_model_to_torque_actuated'):
+        mod.convert_model_to_torque_actuated = lambda *a, **k: None
+    env = getattr(mod, clsname)(config)
+    return env, pk
+
+
+DEFAULT_CFG = dict(visualize=False, max_actuation=200, mode='train', log=False, r_weights=[0.8, 0.2, 0.1],
+                   apply_perturbations=False, use_target_obs=True, use_GRF=True, horizon=5)
+
+
+def seed_for_index(target, hi):
+    for s in range(100000):
+        random.seed(s)
+        if random.randint(0, hi) == target:
+            return s
+    raise RuntimeError
+
+
+def run_episode(env, pk, seed, T, action_fn, nan_at=()):
+    random.seed(seed)
+    obs0 = np.array(env.reset(), dtype=np.float64)
+    index = int(round(CURRENT['reset_time'] / 0.01))
+    acts, obs, rew, done, info = [], [], [], [], []
+    for t in range(T):
+        a = action_fn(t, env)
+        if t in nan_at:
+            a = a.copy()
+            a[0] = np.nan
+        o, r, d, inf = env.step(a)
+        acts.append(a)
+        obs.append(np.asarray(o, dtype=np.float64))
+        rew.append(float(r))
+        done.append(bool(d))
+        info.append(np.asarray(inf['all_rewards'], dtype=np.float64))
+        if d:
+            break
+    return dict(index=index, obs0=obs0, actions=np.array(acts), obs=np.array(obs), reward=np.array(rew),
+                done=np.array(done), info=np.array(info))
+
+
+def main():
+    out = {}
+    # ---------------- MuscleWalkingImitation2D-v0
+    mod = 'bioimitation.imitation_envs.envs.muscle.planar.muscle_walking_imitation_env2D'
+    rng = np.random.Generator(np.random.PCG64(0))
+    eps = []
+    for k, (index, T, nan_at, cfg) in enumerate([(29, 12, (), {}), (None, 40, (7,), {}), (0, 10, (), {'mode': 'test'}),
+                                                  (117, 25, (), {'horizon': 3, 'r_weights': [0.5, 0.3, 0.2]})]):
+        config = dict(DEFAULT_CFG, **cfg)
+        env, pk = make_env('MuscleWalkingImitation2D-v0', mod, 'MuscleWalkingImitationEnv2D', config)
+        seed = 1000 + k if index is None else seed_for_index(index, 132)
+        acts = rng.uniform(0.0, 1.0, size=(T, pk.nact))
+        ep = run_episode(env, pk, seed, T, lambda t, e: acts[t].copy(), nan_at)
+        ep['config'] = repr(config)
+        eps.append(ep)
+        print('muscle episode', k, 'index', ep['index'], 'steps', len(ep['reward']), 'done', ep['done'][-1])
+    # two consecutive episodes on one env: old_pos_pelvisx and the deque persist across reset
+    config = dict(DEFAULT_CFG)
+    env, pk = make_env('MuscleWalkingImitation2D-v0', mod, 'MuscleWalkingImitationEnv2D', config)
+    acts = rng.uniform(0.0, 1.0, size=(16, pk.nact))
+    e1 = run_episode(env, pk, seed_for_index(60, 132), 8, lambda t, e: acts[t].copy())
+    e2 = run_episode(env, pk, seed_for_index(61, 132), 8, lambda t, e: acts[8 + t].copy())
+    e1['config'] = e2['config'] = repr(config)
+    e2['chained'] = 1
+    eps += [e1, e2]
+    out['MuscleWalkingImitation2D-v0'] = eps
+
+    # ---------------- TorqueWalkingImitation2D-v0
+    mod = 'bioimitation.imitation_envs.envs.torque.planar.torque_walking_imitation_env2D'
+    eps = []
+    pdc = registry.PD_COORDS_2D
+    for k, (index, T, nan_at, cfg) in enumerate([(58, 12, (), {}), (None, 40, (9,), {}), (0, 10, (), {'mode': 'test'})]):
+        config = dict(DEFAULT_CFG, **cfg)
+        env, pk = make_env('TorqueWalkingImitation2D-v0', mod, 'TorqueWalkingImitationEnv2D', config)
+        seed = 2000 + k if index is None else seed_for_index(index, 132)
+        noise = rng.normal(0.0, 0.05, size=(T, pk.nact))
+        names = CURRENT['names']['coords']
+
+        def act(t, e, noise=noise, names=names):
+            # PD targets: reference row istep+1 plus N(0, 0.05 rad)
+            row = e.q_d.iloc[min(e.osim_model.istep + 1, len(e.q_d) - 1)]
+            return np.array([row[c] for c in pdc]) + noise[t]
+        ep = run_episode(env, pk, seed, T, act, nan_at)
+        ep['config'] = repr(config)
+        eps.append(ep)
+        print('torque episode', k, 'index', ep['index'], 'steps', len(ep['reward']), 'done', ep['done'][-1])
+    out['TorqueWalkingImitation2D-v0'] = eps
+
+    for env_id, eps in out.items():
+        flat = {}
+        for i, ep in enumerate(eps):
+            for k, v in ep.items():
+                flat[f'ep{i}_{k}'] = np.asarray(v)
+        flat['n_episodes'] = np.array(len(eps))
+        path = os.path.join(HERE, f'{env_id}.npz')
+        np.savez_compressed(path, **flat)
+        print('wrote', path)
+
+
+if __name__ == '__main__':
+    main()
