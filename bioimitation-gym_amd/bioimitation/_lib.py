@@ -1,0 +1,65 @@
+"""ctypes binding of libbioim.so (include/bioim.h), the HIP product path.
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc,
+--offload-arch=gfx950) into ``bioimitation-gym_amd/build/libbioim.so``.  There
+is no CPU fallback: if the library or a GPU is missing, every constructor
+raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import packdef as P
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get('BIOIM_LIB', os.path.join(PKG_ROOT, 'build', 'libbioim.so'))
+
+EXPORTS = ['bioim_create', 'bioim_destroy', 'bioim_reset', 'bioim_step', 'bioim_set_auto_reset', 'bioim_state_dim',
+           'bioim_get_state', 'bioim_set_state', 'bioim_query', 'bioim_stream', 'bioim_set_stream', 'bioim_sync',
+           'bioim_last_error', 'bioim_modelpack_size']
+
+_lib = None
+
+
+class BioimError(RuntimeError):
+    pass
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise BioimError(f'libbioim.so not found at {LIB_PATH}; run __graft_entry__.build()')
+    L = C.CDLL(LIB_PATH)
+    vp, i32p, dp = C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_double)
+    sig = {
+        'bioim_create': (C.c_int, [C.POINTER(P.ModelPack), C.c_int, C.c_int, C.c_int, C.c_uint64, C.POINTER(vp)]),
+        'bioim_destroy': (C.c_int, [vp]),
+        'bioim_reset': (C.c_int, [vp, vp, vp, C.c_int, vp]),
+        'bioim_step': (C.c_int, [vp, vp, vp, vp, vp, vp]),
+        'bioim_set_auto_reset': (C.c_int, [vp, C.c_int]),
+        'bioim_state_dim': (C.c_int, [vp]),
+        'bioim_get_state': (C.c_int, [vp, dp]),
+        'bioim_set_state': (C.c_int, [vp, dp]),
+        'bioim_query': (C.c_int, [vp, i32p]),
+        'bioim_stream': (vp, [vp]),
+        'bioim_set_stream': (C.c_int, [vp, vp]),
+        'bioim_sync': (C.c_int, [vp]),
+        'bioim_last_error': (C.c_char_p, []),
+        'bioim_modelpack_size': (C.c_uint64, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    if L.bioim_modelpack_size() != C.sizeof(P.ModelPack):
+        raise BioimError('ModelPack layout mismatch between libbioim.so and packdef.py')
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc < 0:
+        raise BioimError(_lib.bioim_last_error().decode())
+    return rc

@@ -1,0 +1,106 @@
+"""Batched env over the HIP C-ABI: N environments of one registered ID on
+one GPU, stepped by one kernel launch.
+
+This is the throughput surface (RLlib ``VectorEnv`` / gym vector-env shaped);
+:class:`bioimitation.envs.ImitationEnv` is the single-instance, reference-
+shaped surface built on top of it.  Buffers are torch tensors on the GPU;
+the kernel runs on torch's current stream of that device so it orders with
+the caller's torch work.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .registry import load_pack
+
+
+class VectorEnv:
+    def __init__(self, env_id: str, num_envs: int, config: dict = None, device: int = 0, precision: int = 32,
+                 seed: int = 0, auto_reset: bool = False):
+        import torch
+        if not torch.cuda.is_available():
+            raise _lib.BioimError('VectorEnv needs a HIP GPU (no CPU fallback)')
+        L = _lib.load()
+        self.env_id = env_id
+        self.pack = load_pack(env_id, config)
+        self.num_envs = int(num_envs)
+        self.device = torch.device('cuda', device)
+        self.precision = precision
+        self.dtype = torch.float32 if precision == 32 else torch.float64
+        h = C.c_void_p()
+        _lib.check(L.bioim_create(C.byref(self.pack), self.num_envs, device, precision, seed, C.byref(h)))
+        self._h = h
+        self._L = L
+        with torch.cuda.device(self.device):
+            _lib.check(L.bioim_set_stream(h, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+        q = (C.c_int32 * 8)()
+        _lib.check(L.bioim_query(h, q))
+        self.obs_dim, self.action_dim, self.info_dim, self.lanes_per_env, self.nsub, self.state_dim = \
+            q[1], q[2], q[3], q[5], q[6], q[7]
+        _lib.check(L.bioim_set_auto_reset(h, 1 if auto_reset else 0))
+        n = self.num_envs
+        self.obs = torch.zeros((n, self.obs_dim), dtype=self.dtype, device=self.device)
+        self.reward = torch.zeros(n, dtype=self.dtype, device=self.device)
+        self.done = torch.zeros(n, dtype=torch.uint8, device=self.device)
+        self.info = torch.zeros((n, self.info_dim), dtype=self.dtype, device=self.device)
+
+    @staticmethod
+    def _ptr(t):
+        return C.c_void_p(t.data_ptr()) if t is not None else None
+
+    def set_auto_reset(self, on: bool):
+        _lib.check(self._L.bioim_set_auto_reset(self._h, 1 if on else 0))
+
+    def reset(self, env_ids=None, ref_index=None):
+        """Reset the listed envs (default all).  ref_index: reference rows
+        (default: randint(0, reset_hi) drawn on the device)."""
+        import torch
+        ids = rows = None
+        n = self.num_envs
+        if env_ids is not None:
+            ids = torch.as_tensor(env_ids, dtype=torch.int32, device=self.device).contiguous()
+            n = ids.numel()
+        if ref_index is not None:
+            rows = torch.as_tensor(ref_index, dtype=torch.int32, device=self.device).contiguous()
+            if ids is None:
+                ids = torch.arange(self.num_envs, dtype=torch.int32, device=self.device)
+            assert rows.numel() == n
+        _lib.check(self._L.bioim_reset(self._h, self._ptr(ids), self._ptr(rows), n, self._ptr(self.obs)))
+        return self.obs
+
+    def step(self, actions):
+        """actions: (N, nact) tensor on the env's device (dtype = precision)."""
+        a = actions
+        if a.dtype != self.dtype or a.device != self.device or not a.is_contiguous():
+            a = a.to(device=self.device, dtype=self.dtype).contiguous()
+        assert a.shape == (self.num_envs, self.action_dim), a.shape
+        _lib.check(self._L.bioim_step(self._h, self._ptr(a), self._ptr(self.obs), self._ptr(self.reward),
+                                      self._ptr(self.done), self._ptr(self.info)))
+        return self.obs, self.reward, self.done, self.info
+
+    def get_state(self) -> np.ndarray:
+        s = np.zeros((self.num_envs, self.state_dim))
+        _lib.check(self._L.bioim_get_state(self._h, s.ctypes.data_as(C.POINTER(C.c_double))))
+        return s
+
+    def set_state(self, s: np.ndarray):
+        s = np.ascontiguousarray(s, dtype=np.float64)
+        assert s.shape == (self.num_envs, self.state_dim)
+        _lib.check(self._L.bioim_set_state(self._h, s.ctypes.data_as(C.POINTER(C.c_double))))
+
+    def sync(self):
+        _lib.check(self._L.bioim_sync(self._h))
+
+    def close(self):
+        if getattr(self, '_h', None):
+            self._L.bioim_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,1745 @@
+// bioim_step.hip — MI355X (gfx950) batched env step for bioimitation-gym.
+//
+// One launch advances N environments by one env step (0.01 s): action
+// pre-processing, nsub semi-implicit substeps of the musculoskeletal
+// forward dynamics, the realize at the end state, and the observation,
+// reward and termination of the reference's task envs.
+//
+// Work decomposition (CDNA4, wave64): an environment is a group of G lanes
+// (G = 16 for the 2D models: 4 envs per wave, 16 per 256-thread workgroup).
+//   - the multibody part (kinematics, composite-rigid-body mass matrix,
+//     Newton-Euler bias, contact, limits, Cholesky) is computed redundantly
+//     by every lane of the group, fully unrolled against the compile-time
+//     topology (topologies.h) so all of it lives in VGPRs;
+//   - muscle m runs on lane m (path geometry, Millard damped equilibrium,
+//     activation), and the generalized forces are summed across the group
+//     with xor-shuffles;
+//   - body frames and coordinates that muscle lanes index at run time are
+//     staged in LDS (one region per env).
+// Model constants are wave-uniform (scalar loads); per-env state is SoA in
+// HBM (env index fastest).  Reference semantics: see oracle/bioim_oracle.c,
+// which this kernel must match (tests/test_gpu_parity.py).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "bioim.h"
+#include "bioim_device.h"
+#include "topologies.h"
+
+#define DEV __device__ __forceinline__
+
+template <int I, int N, class F>
+DEV void sfor(F &&f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        sfor<I + 1, N>(f);
+    }
+}
+
+template <typename Real> struct Eps;
+template <> struct Eps<float> {
+    static constexpr float u_tol = 2e-7f;   /* Bezier parameter tolerance  */
+    static constexpr float v_tol = 1e-7f;   /* normalized velocity         */
+    static constexpr float l_tol = 1e-9f;   /* fiber length (m)            */
+    static constexpr int it_max = 24;
+};
+template <> struct Eps<double> {
+    static constexpr double u_tol = 1e-15;
+    static constexpr double v_tol = 1e-15;
+    static constexpr double l_tol = 1e-15;
+    static constexpr int it_max = 60;
+};
+
+/* ------------------------------------------------------------- vec3 */
+template <typename Real> DEV void cross3(const Real *a, const Real *b, Real *o) {
+    Real x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+template <typename Real> DEV Real dot3(const Real *a, const Real *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+template <typename Real> DEV void mv3(const Real *R, const Real *v, Real *o) {
+    Real x = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
+    Real y = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
+    Real z = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+template <typename Real> DEV void mm3(const Real *A, const Real *B, Real *C) {
+    Real T[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) T[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) C[i] = T[i];
+}
+template <typename Real> DEV void axis_rot(const Real *a, Real th, Real *R) {
+    Real s, c;
+    s = sin(th);
+    c = cos(th);
+    Real t = Real(1) - c, x = a[0], y = a[1], z = a[2];
+    R[0] = t * x * x + c;     R[1] = t * x * y - s * z; R[2] = t * x * z + s * y;
+    R[3] = t * x * y + s * z; R[4] = t * y * y + c;     R[5] = t * y * z - s * x;
+    R[6] = t * x * z - s * y; R[7] = t * y * z + s * x; R[8] = t * z * z + c;
+}
+
+template <int G, typename Real> DEV Real group_sum(Real x) {
+#pragma unroll
+    for (int off = G / 2; off >= 1; off >>= 1) x += __shfl_xor(x, off, G);
+    return x;
+}
+template <int G> DEV bool group_any(bool p) {
+    unsigned long long b = __ballot(p);
+    int base = (threadIdx.x & 63) & ~(G - 1);
+    unsigned long long m = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+    return ((b >> base) & m) != 0ull;
+}
+
+/* ------------------------------------------------------------ functions */
+template <typename Real>
+DEV void spline_eval(const DModel<Real> &M, int off, int n, Real q, Real &f, Real &f1, Real &f2) {
+    Real x0 = M.kx[off], xn = M.kx[off + n - 1];
+    if (q < x0) { f = M.ky[off] + (q - x0) * M.kb[off]; f1 = M.kb[off]; f2 = 0; return; }
+    if (q > xn) {
+        int j = off + n - 1;
+        f = M.ky[j] + (q - xn) * M.kb[j]; f1 = M.kb[j]; f2 = 0; return;
+    }
+    int k = 0;
+    for (int i = 1; i < n - 1; ++i) k += (q > M.kx[off + i]) ? 1 : 0;
+    int j = off + k;
+    Real dx = q - M.kx[j], b = M.kb[j], c = M.kc[j], d = M.kd[j];
+    f = M.ky[j] + dx * (b + dx * (c + dx * d));
+    f1 = b + dx * (Real(2) * c + Real(3) * dx * d);
+    f2 = Real(2) * c + Real(6) * dx * d;
+}
+
+/* runtime-kind evaluation (moving path points) */
+template <typename Real>
+DEV void fn_eval_rt(const DModel<Real> &M, int fi, Real q, Real &f, Real &f1, Real &f2) {
+    int type = M.fn_type[fi];
+    if (type == BIOIM_FN_CONST) { f = M.fn_b[fi]; f1 = 0; f2 = 0; }
+    else if (type == BIOIM_FN_LINEAR) { f = M.fn_a[fi] * q + M.fn_b[fi]; f1 = M.fn_a[fi]; f2 = 0; }
+    else {
+        Real s, s1, s2;
+        spline_eval(M, M.fn_off[fi], M.fn_n[fi], q, s, s1, s2);
+        Real a = M.fn_a[fi];
+        f = a * s; f1 = a * s1; f2 = a * s2;
+    }
+}
+
+template <int KIND, typename Real>
+DEV void fn_eval_ct(const DModel<Real> &M, int fi, Real q, Real &f, Real &f1, Real &f2) {
+    if constexpr (KIND == BIOIM_FN_CONST) { f = M.fn_b[fi]; f1 = 0; f2 = 0; }
+    else if constexpr (KIND == BIOIM_FN_LINEAR) { f = M.fn_a[fi] * q + M.fn_b[fi]; f1 = M.fn_a[fi]; f2 = 0; }
+    else {
+        Real s, s1, s2;
+        spline_eval(M, M.fn_off[fi], M.fn_n[fi], q, s, s1, s2);
+        Real a = M.fn_a[fi];
+        f = a * s; f1 = a * s1; f2 = a * s2;
+    }
+}
+
+/* ----------------------------------------------------- smooth curves */
+template <typename Real> DEV Real bez5(const Real *p, Real u) {
+    Real v = Real(1) - u, u2 = u * u, v2 = v * v;
+    return p[0] * v2 * v2 * v + Real(5) * p[1] * u * v2 * v2 + Real(10) * p[2] * u2 * v2 * v +
+           Real(10) * p[3] * u2 * u * v2 + Real(5) * p[4] * u2 * u2 * v + p[5] * u2 * u2 * u;
+}
+template <typename Real> DEV Real dbez5(const Real *p, Real u) {
+    Real v = Real(1) - u, u2 = u * u, v2 = v * v;
+    return Real(5) * ((p[1] - p[0]) * v2 * v2 + Real(4) * (p[2] - p[1]) * u * v2 * v +
+                      Real(6) * (p[3] - p[2]) * u2 * v2 + Real(4) * (p[4] - p[3]) * u2 * u * v + (p[5] - p[4]) * u2 * u2);
+}
+
+/* y(x), dy/dx: segment located branch-free, x(u) inverted by bracketed Newton */
+template <typename Real>
+DEV void curve_eval(const DCurve<Real> &C, Real x, Real &y, Real &dydx) {
+    if (x <= C.x0) { y = C.y0 + C.dydx0 * (x - C.x0); dydx = C.dydx0; return; }
+    if (x >= C.x1) { y = C.y1 + C.dydx1 * (x - C.x1); dydx = C.dydx1; return; }
+    int k = 0;
+    for (int s = 0; s < C.nseg - 1; ++s) k += (x > C.x[s][5]) ? 1 : 0;
+    Real px[6], py[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) { px[i] = C.x[k][i]; py[i] = C.y[k][i]; }
+    Real lo = 0, hi = 1, u = (x - px[0]) / (px[5] - px[0]);
+    for (int it = 0; it < Eps<Real>::it_max; ++it) {
+        Real f = bez5(px, u) - x;
+        if (f > 0) hi = u; else lo = u;
+        Real d = dbez5(px, u);
+        Real un = u - f / d;
+        if (!(un > lo && un < hi)) un = Real(0.5) * (lo + hi);
+        Real du = un - u;
+        u = un;
+        if (fabs(du) <= Eps<Real>::u_tol) break;
+    }
+    y = bez5(py, u);
+    dydx = dbez5(py, u) / dbez5(px, u);
+}
+
+/* root of a*fal*fv(v) + beta*v = rhs (increasing in v), solved directly in
+ * the Bezier parameter of the bracketing segment; returns v, fv, dfv/dv */
+template <typename Real>
+DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real &v, Real &fv, Real &dfv) {
+    Real g0 = afal * C.y0 + beta * C.x0 - rhs;
+    if (g0 >= 0) {
+        v = (rhs - afal * (C.y0 - C.dydx0 * C.x0)) / (afal * C.dydx0 + beta);
+        fv = C.y0 + C.dydx0 * (v - C.x0); dfv = C.dydx0; return;
+    }
+    Real g1 = afal * C.y1 + beta * C.x1 - rhs;
+    if (g1 <= 0) {
+        v = (rhs - afal * (C.y1 - C.dydx1 * C.x1)) / (afal * C.dydx1 + beta);
+        fv = C.y1 + C.dydx1 * (v - C.x1); dfv = C.dydx1; return;
+    }
+    int k = 0;
+    for (int s = 1; s < C.nseg; ++s) k += (afal * C.y[s][0] + beta * C.x[s][0] - rhs <= 0) ? 1 : 0;
+    Real px[6], py[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) { px[i] = C.x[k][i]; py[i] = C.y[k][i]; }
+    Real ga = afal * py[0] + beta * px[0] - rhs, gb = afal * py[5] + beta * px[5] - rhs;
+    Real lo = 0, hi = 1, u = ga / (ga - gb);
+    for (int it = 0; it < Eps<Real>::it_max; ++it) {
+        Real g = afal * bez5(py, u) + beta * bez5(px, u) - rhs;
+        if (g > 0) hi = u; else lo = u;
+        Real dg = afal * dbez5(py, u) + beta * dbez5(px, u);
+        Real un = u - g / dg;
+        if (!(un > lo && un < hi)) un = Real(0.5) * (lo + hi);
+        Real du = un - u;
+        u = un;
+        if (fabs(du) <= Eps<Real>::u_tol) break;
+    }
+    v = bez5(px, u);
+    fv = bez5(py, u);
+    dfv = dbez5(py, u) / dbez5(px, u);
+}
+
+/* ---------------------------------------------------------- kinematics */
+template <typename Real> struct Kin {
+    Real R[9], o[3], w[3], vO[3], al[3], aO[3];
+};
+
+template <class T, typename Real> struct Work {
+    static constexpr int ND = T::ND > 0 ? T::ND : 1;
+    static constexpr int NP = ND * (ND + 1) / 2;
+    Kin<Real> K[T::NB];
+    Real S[ND][6];
+    Real qf[T::NC], uf[T::NC];
+};
+
+template <int I> DEV constexpr int tri(int k, int l) { return k * (k + 1) / 2 + l; }
+
+template <class T, typename Real>
+DEV void fill_coords(const DModel<Real> &M, const Real *q, const Real *u, Work<T, Real> &W) {
+    sfor<0, T::NC>([&](auto cI) {
+        constexpr int c = decltype(cI)::value;
+        constexpr int d = T::coord_dof[c];
+        if constexpr (d >= 0) { W.qf[c] = q[d]; W.uf[c] = u[d]; }
+        else { W.qf[c] = M.coord_default[c]; W.uf[c] = 0; }
+    });
+}
+
+template <class T, typename Real>
+DEV void kinematics(const DModel<Real> &M, Work<T, Real> &W) {
+    sfor<0, T::NB>([&](auto cI) {
+        constexpr int c = decltype(cI)::value;
+        constexpr int p = T::parent[c];
+        Kin<Real> &k = W.K[c];
+        Real RP[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, oP[3] = {0, 0, 0}, wP[3] = {0, 0, 0}, vOP[3] = {0, 0, 0},
+             alP[3] = {0, 0, 0}, aOP[3] = {0, 0, 0};
+        if constexpr (p >= 0) {
+#pragma unroll
+            for (int i = 0; i < 9; ++i) RP[i] = W.K[p].R[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                oP[i] = W.K[p].o[i]; wP[i] = W.K[p].w[i]; vOP[i] = W.K[p].vO[i];
+                alP[i] = W.K[p].al[i]; aOP[i] = W.K[p].aO[i];
+            }
+        }
+        Real RGF[9], oF[3], vF[3], aF[3], t[3], t2[3];
+        mm3(RP, M.R_pf[c], RGF);
+        mv3(RP, M.p_pf[c], t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) oF[i] = oP[i] + t[i];
+        cross3(wP, oF, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) vF[i] = vOP[i] + t[i];
+        cross3(alP, oF, t);
+        cross3(wP, vF, t2);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) aF[i] = aOP[i] + t[i] + t2[i];
+
+        Real RFM[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        Real wrel[3] = {0, 0, 0}, arel[3] = {0, 0, 0}, pFM[3] = {0, 0, 0}, pd[3] = {0, 0, 0}, pdd[3] = {0, 0, 0};
+        Real ucol[3][3], f1s[6] = {0, 0, 0, 0, 0, 0};
+        sfor<0, 3>([&](auto aI) {
+            constexpr int ax = decltype(aI)::value;
+            constexpr int kind = T::axis_kind[c * 6 + ax];
+            constexpr int cc = T::axis_coord[c * 6 + ax];
+            mv3(RFM, M.axis[c][ax], ucol[ax]);
+            if constexpr (kind >= 0) {
+                Real qc = 0, uc = 0;
+                if constexpr (cc >= 0) { qc = W.qf[cc]; uc = W.uf[cc]; }
+                Real f, f1, f2;
+                fn_eval_ct<kind>(M, M.fn[c][ax], qc, f, f1, f2);
+                f1s[ax] = f1;
+                Real thd = f1 * uc, cr[3];
+                cross3(wrel, ucol[ax], cr);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) arel[i] += ucol[ax][i] * (f2 * uc * uc) + cr[i] * thd;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) wrel[i] += ucol[ax][i] * thd;
+                Real Rk[9];
+                axis_rot(M.axis[c][ax], f, Rk);
+                mm3(RFM, Rk, RFM);
+            }
+        });
+        sfor<3, 6>([&](auto aI) {
+            constexpr int ax = decltype(aI)::value;
+            constexpr int kind = T::axis_kind[c * 6 + ax];
+            constexpr int cc = T::axis_coord[c * 6 + ax];
+            if constexpr (kind >= 0) {
+                Real qc = 0, uc = 0;
+                if constexpr (cc >= 0) { qc = W.qf[cc]; uc = W.uf[cc]; }
+                Real f, f1, f2;
+                fn_eval_ct<kind>(M, M.fn[c][ax], qc, f, f1, f2);
+                f1s[ax] = f1;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    Real a = M.axis[c][ax][i];
+                    pFM[i] += a * f; pd[i] += a * f1 * uc; pdd[i] += a * f2 * uc * uc;
+                }
+            }
+        });
+        Real wr[3], ar[3], r[3], rd[3], rdd[3];
+        mv3(RGF, wrel, wr);
+        mv3(RGF, arel, ar);
+        mv3(RGF, pFM, r);
+        mv3(RGF, pd, rd);
+        mv3(RGF, pdd, rdd);
+        Real w[3], al[3], oM[3], vM[3], aM[3];
+        cross3(wP, wr, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { w[i] = wP[i] + wr[i]; al[i] = alP[i] + t[i] + ar[i]; oM[i] = oF[i] + r[i]; }
+        cross3(wP, r, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) vM[i] = vF[i] + t[i] + rd[i];
+        {
+            Real a1[3], a2[3], a3[3], wr2[3];
+            cross3(alP, r, a1);
+            cross3(wP, r, wr2);
+            cross3(wP, wr2, a2);
+            cross3(wP, rd, a3);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) aM[i] = aF[i] + a1[i] + a2[i] + Real(2) * a3[i] + rdd[i];
+        }
+        Real RGM[9], dd[3], oB[3], vB[3], aB[3];
+        mm3(RGF, RFM, RGM);
+        mm3(RGM, M.R_mb[c], k.R);
+        mv3(RGM, M.p_mb[c], dd);
+        cross3(w, dd, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { oB[i] = oM[i] + dd[i]; vB[i] = vM[i] + t[i]; }
+        {
+            Real a1[3], a2[3], wd[3];
+            cross3(al, dd, a1);
+            cross3(w, dd, wd);
+            cross3(w, wd, a2);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) aB[i] = aM[i] + a1[i] + a2[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { k.o[i] = oB[i]; k.w[i] = w[i]; k.al[i] = al[i]; }
+        cross3(w, oB, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) k.vO[i] = vB[i] - t[i];
+        {
+            Real a1[3], a2[3];
+            cross3(al, oB, a1);
+            cross3(w, vB, a2);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) k.aO[i] = aB[i] - a1[i] - a2[i];
+        }
+        /* Plucker columns of the dofs of this joint */
+        sfor<0, T::ND>([&](auto dI) {
+            constexpr int d = decltype(dI)::value;
+            if constexpr (T::dof_cb[d] == c) {
+                constexpr int cc = T::dof_coord[d];
+                Real Om[3] = {0, 0, 0}, Vm[3] = {0, 0, 0};
+                sfor<0, 3>([&](auto aI) {
+                    constexpr int ax = decltype(aI)::value;
+                    if constexpr (T::axis_coord[c * 6 + ax] == cc && T::axis_kind[c * 6 + ax] >= 0) {
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) Om[i] += ucol[ax][i] * f1s[ax];
+                    }
+                });
+                sfor<3, 6>([&](auto aI) {
+                    constexpr int ax = decltype(aI)::value;
+                    if constexpr (T::axis_coord[c * 6 + ax] == cc && T::axis_kind[c * 6 + ax] >= 0) {
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) Vm[i] += M.axis[c][ax][i] * f1s[ax];
+                    }
+                });
+                Real OG[3], VG[3], tt[3];
+                mv3(RGF, Om, OG);
+                mv3(RGF, Vm, VG);
+                cross3(OG, oM, tt);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) { W.S[d][i] = OG[i]; W.S[d][3 + i] = VG[i] - tt[i]; }
+            }
+        });
+    });
+}
+
+/* velocity of the material point of composite c at ground point P */
+template <typename Real> DEV void point_vel(const Kin<Real> &k, const Real *P, Real *v) {
+    Real t[3];
+    cross3(k.w, P, t);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) v[i] = k.vO[i] + t[i];
+}
+
+/* tau += J_P^T F for a point force on composite c (dofs in dofmask[c]) */
+template <class T, int C, typename Real>
+DEV void point_force(const Work<T, Real> &W, const Real *P, const Real *F, Real *tau) {
+    Real m[3];
+    cross3(P, F, m);
+    sfor<0, T::ND>([&](auto dI) {
+        constexpr int d = decltype(dI)::value;
+        if constexpr ((T::dofmask[C] >> d) & 1u) tau[d] += dot3(W.S[d], m) + dot3(W.S[d] + 3, F);
+    });
+}
+
+/* ------------------------------------------------ mass matrix and bias */
+template <class T, typename Real>
+DEV void mass_bias(const DModel<Real> &M, const Work<T, Real> &W, Real *Mp, Real *bias) {
+    constexpr int NB = T::NB;
+    Real Jc[NB][9], hc[NB][3], mc[NB], Wn[NB][3], Wf[NB][3];
+    sfor<0, NB>([&](auto cI) {
+        constexpr int c = decltype(cI)::value;
+        const Kin<Real> &k = W.K[c];
+        Real cl[3], cG[3];
+        mv3(k.R, M.com[c], cl);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) cG[i] = k.o[i] + cl[i];
+        /* IG = R Ib R^T */
+        Real Ib[9] = {M.inertia[c][0], M.inertia[c][3], M.inertia[c][4], M.inertia[c][3], M.inertia[c][1],
+                      M.inertia[c][5], M.inertia[c][4], M.inertia[c][5], M.inertia[c][2]};
+        Real Tm[9], RT[9], IG[9];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) RT[3 * i + j] = k.R[3 * j + i];
+        mm3(k.R, Ib, Tm);
+        mm3(Tm, RT, IG);
+        Real m = M.mass[c];
+        mc[c] = m;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) hc[c][i] = m * cG[i];
+        Real cc = dot3(cG, cG);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) Jc[c][3 * i + j] = IG[3 * i + j] + m * ((i == j ? cc : Real(0)) - cG[i] * cG[j]);
+        Real vc[3], ac[3], t[3], t2[3];
+        cross3(k.w, cG, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) vc[i] = k.vO[i] + t[i];
+        cross3(k.al, cG, t);
+        cross3(k.w, vc, t2);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) ac[i] = k.aO[i] + t[i] + t2[i];
+        Real f[3], Iw[3], Ia[3], n[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) f[i] = m * (ac[i] - M.gravity[i]);
+        mv3(IG, k.w, Iw);
+        mv3(IG, k.al, Ia);
+        cross3(k.w, Iw, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) n[i] = Ia[i] + t[i];
+        cross3(cG, f, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { Wn[c][i] = n[i] + t[i]; Wf[c][i] = f[i]; }
+    });
+    sfor<0, NB>([&](auto iI) {
+        constexpr int c = NB - 1 - decltype(iI)::value;
+        constexpr int p = T::parent[c];
+        if constexpr (p >= 0) {
+            mc[p] += mc[c];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { hc[p][i] += hc[c][i]; Wn[p][i] += Wn[c][i]; Wf[p][i] += Wf[c][i]; }
+#pragma unroll
+            for (int i = 0; i < 9; ++i) Jc[p][i] += Jc[c][i];
+        }
+    });
+    sfor<0, T::ND>([&](auto dI) {
+        constexpr int d = decltype(dI)::value;
+        constexpr int c = T::dof_cb[d];
+        bias[d] = dot3(W.S[d], Wn[c]) + dot3(W.S[d] + 3, Wf[c]);
+    });
+    sfor<0, T::ND>([&](auto lI) {
+        constexpr int l = decltype(lI)::value;
+        constexpr int cl = T::dof_cb[l];
+        const Real *Sl = W.S[l];
+        /* momentum of the composite below l's body per unit u_l */
+        Real L[3], Pm[3], t[3];
+        mv3(Jc[cl], Sl, L);
+        cross3(hc[cl], Sl + 3, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) L[i] += t[i];
+        cross3(Sl, hc[cl], t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) Pm[i] = mc[cl] * Sl[3 + i] + t[i];
+        sfor<0, l + 1>([&](auto kI) {
+            constexpr int k = decltype(kI)::value;
+            constexpr int ck = T::dof_cb[k];
+            if constexpr ((T::anc[cl] >> ck) & 1u) {
+                Mp[tri<0>(l, k)] = dot3(W.S[k], L) + dot3(W.S[k] + 3, Pm);
+            } else if constexpr ((T::anc[ck] >> cl) & 1u) {
+                /* cl is an ancestor of ck (k < l cannot be deeper in a topological
+                 * dof order unless on another branch) — computed from ck's side */
+                Real L2[3], P2[3], t3[3];
+                const Real *Sk = W.S[k];
+                mv3(Jc[ck], Sk, L2);
+                cross3(hc[ck], Sk + 3, t3);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) L2[i] += t3[i];
+                cross3(Sk, hc[ck], t3);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) P2[i] = mc[ck] * Sk[3 + i] + t3[i];
+                Mp[tri<0>(l, k)] = dot3(Sl, L2) + dot3(Sl + 3, P2);
+            } else {
+                Mp[tri<0>(l, k)] = 0;
+            }
+        });
+    });
+}
+
+/* in-place packed-lower Cholesky solve; returns false if not SPD */
+template <int N, typename Real> DEV bool cholesky_solve(Real *A, Real *b) {
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        Real s = A[tri<0>(j, j)];
+#pragma unroll
+        for (int k = 0; k < j; ++k) s -= A[tri<0>(j, k)] * A[tri<0>(j, k)];
+        ok = ok && (s > 0);
+        Real d = sqrt(s > 0 ? s : Real(1e-30));
+        Real inv = Real(1) / d;
+        A[tri<0>(j, j)] = d;
+#pragma unroll
+        for (int i = j + 1; i < N; ++i) {
+            Real t = A[tri<0>(i, j)];
+#pragma unroll
+            for (int k = 0; k < j; ++k) t -= A[tri<0>(i, k)] * A[tri<0>(j, k)];
+            A[tri<0>(i, j)] = t * inv;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        Real t = b[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) t -= A[tri<0>(i, k)] * b[k];
+        b[i] = t / A[tri<0>(i, i)];
+    }
+#pragma unroll
+    for (int i = N - 1; i >= 0; --i) {
+        Real t = b[i];
+#pragma unroll
+        for (int k = i + 1; k < N; ++k) t -= A[tri<0>(k, i)] * b[k];
+        b[i] = t / A[tri<0>(i, i)];
+    }
+    return ok;
+}
+
+/* ---------------------------------------------------- contact + limits */
+template <typename Real> DEV Real smooth_step(Real y0, Real y1, Real x0, Real x1, Real x) {
+    if (x <= x0) return y0;
+    if (x >= x1) return y1;
+    Real t = (x - x0) / (x1 - x0);
+    return y0 + (y1 - y0) * t * t * t * (Real(10) + t * (Real(6) * t - Real(15)));
+}
+template <typename Real> DEV Real smooth_step_d(Real y0, Real y1, Real x0, Real x1, Real x) {
+    if (x <= x0 || x >= x1) return 0;
+    Real w = x1 - x0, t = (x - x0) / w;
+    return (y1 - y0) * Real(30) * t * t * (Real(1) - t) * (Real(1) - t) / w;
+}
+
+template <class T, typename Real> struct Contact {
+    Real F[T::NF > 0 ? T::NF : 1][3], Mo[T::NF > 0 ? T::NF : 1][3];
+};
+
+/* Hunt-Crossley spheres vs ground plane; h > 0 adds the implicit terms */
+template <class T, typename Real>
+DEV void contact_all(const DModel<Real> &M, const Work<T, Real> &W, Real *tau, Real *Mp, Real h, Contact<T, Real> &co) {
+    sfor<0, T::NF>([&](auto fI) {
+        constexpr int f = decltype(fI)::value;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { co.F[f][i] = 0; co.Mo[f][i] = 0; }
+    });
+    sfor<0, T::NS>([&](auto sI) {
+        constexpr int s = decltype(sI)::value;
+        constexpr int cb = T::sphere_cb[s];
+        constexpr int fo = T::sphere_force[s];
+        const Kin<Real> &k = W.K[cb];
+        Real Cn[3];
+        mv3(k.R, M.sph_loc[s], Cn);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) Cn[i] += k.o[i];
+        Real rad = M.sph_r[s];
+        Real depth = rad - Cn[1];
+        if (depth > 0) {
+            Real P[3] = {Cn[0], Cn[1] - (rad - Real(0.5) * depth), Cn[2]};
+            Real vs[3];
+            point_vel(k, P, vs);
+            Real vn = -vs[1];
+            Real kk = M.cf_kk[fo], cdis = M.cf_c[fo];
+            Real fH = Real(4.0 / 3.0) * kk * depth * sqrt(rad * kk * depth);
+            Real fn = fH * (Real(1) + Real(1.5) * cdis * vn);
+            if (fn > 0) {
+                Real F[3] = {0, fn, 0};
+                Real vt0 = -vs[0], vt2 = -vs[2];
+                Real vslip = sqrt(vt0 * vt0 + vt2 * vt2);
+                Real vtr = M.cf_vt[fo], ms = M.cf_ms[fo], md = M.cf_md[fo], mv = M.cf_mv[fo];
+                Real r_ = vslip / vtr, den = Real(1) + r_ * r_;
+                if (vslip != 0) {
+                    Real ff = fn * (fmin(r_, Real(1)) * (md + Real(2) * (ms - md) / den) + mv * vslip);
+                    F[0] += ff * vt0 / vslip;
+                    F[2] += ff * vt2 / vslip;
+                }
+                point_force<T, cb>(W, P, F, tau);
+                Real mo[3];
+                cross3(P, F, mo);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) { co.F[fo][i] += F[i]; co.Mo[fo][i] += mo[i]; }
+                if (h > 0) {
+                    Real g_s, gp;
+                    if (r_ < 1) {
+                        g_s = (md + Real(2) * (ms - md) / den) / vtr + mv;
+                        gp = (md + Real(2) * (ms - md) / den) / vtr - Real(4) * (ms - md) * r_ * r_ / (den * den * vtr) + mv;
+                    } else {
+                        g_s = (md + Real(2) * (ms - md) / den) / vslip + mv;
+                        gp = -Real(4) * (ms - md) * r_ / (den * den * vtr) + mv;
+                    }
+                    gp = gp < 0 ? Real(0) : gp;
+                    Real tx = 0, tz = 0;
+                    if (vslip > 0) { tx = vt0 / vslip; tz = vt2 / vslip; }
+                    Real ct = h * fn * g_s, cq = h * fn * (gp - g_s);
+                    Real kn = Real(1.5) * fH / depth * (Real(1) + Real(1.5) * cdis * vn);
+                    Real cnn = h * Real(1.5) * cdis * fH + h * h * kn;
+                    Real C3[9] = {ct + cq * tx * tx, 0, cq * tx * tz, 0, cnn, 0, cq * tx * tz, 0, ct + cq * tz * tz};
+                    /* point Jacobian columns */
+                    Real jc[T::ND][3];
+                    sfor<0, T::ND>([&](auto dI) {
+                        constexpr int d = decltype(dI)::value;
+                        if constexpr ((T::dofmask[cb] >> d) & 1u) {
+                            cross3(W.S[d], P, jc[d]);
+#pragma unroll
+                            for (int i = 0; i < 3; ++i) jc[d][i] += W.S[d][3 + i];
+                        }
+                    });
+                    sfor<0, T::ND>([&](auto lI) {
+                        constexpr int l = decltype(lI)::value;
+                        if constexpr ((T::dofmask[cb] >> l) & 1u) {
+                            Real cj[3];
+                            mv3(C3, jc[l], cj);
+                            sfor<0, l + 1>([&](auto kI) {
+                                constexpr int kk2 = decltype(kI)::value;
+                                if constexpr ((T::dofmask[cb] >> kk2) & 1u) Mp[tri<0>(l, kk2)] += dot3(jc[kk2], cj);
+                            });
+                        }
+                    });
+                    Real Fk[3] = {0, -h * kn * vs[1], 0};
+                    point_force<T, cb>(W, P, Fk, tau);
+                }
+            }
+        }
+    });
+}
+
+/* ------------------------------------------------------------ muscles */
+template <typename Real> struct MState {
+    Real act, lce, vce, Ft, Ff, Fa, dadt, dvdl;
+    bool clamped;
+};
+
+template <typename Real>
+DEV void muscle_eval(const DMuscle<Real> &mu, Real a_state, Real l_state, Real excitation, Real L, MState<Real> &s) {
+    Real a = a_state < mu.amin ? mu.amin : (a_state > Real(1) ? Real(1) : a_state);
+    Real lce = l_state < mu.lmin ? mu.lmin : l_state;
+    Real w = mu.width;
+    Real sq = sqrt(lce * lce - w * w);
+    Real cosphi = sq / lce;
+    Real lt = L - sq;
+    Real fse, dfse, fal, dfal, fpe, dfpe;
+    curve_eval(mu.fse, lt * mu.inv_lts, fse, dfse);
+    curve_eval(mu.fal, lce * mu.inv_lopt, fal, dfal);
+    curve_eval(mu.fpe, lce * mu.inv_lopt, fpe, dfpe);
+    Real rhs = fse / cosphi - fpe;
+    Real vN, fvv, dfv;
+    solve_fv(mu.fv, a * fal, mu.beta, rhs, vN, fvv, dfv);
+    Real dGdv = a * fal * dfv + mu.beta;
+    bool clamped = (l_state <= mu.lmin && vN <= 0) || l_state < mu.lmin;
+    if (clamped) {
+        vN = 0;
+        Real y, dy;
+        curve_eval(mu.fv, Real(0), y, dy);
+        fvv = y;
+    }
+    s.act = a;
+    s.lce = lce;
+    s.vce = vN * mu.lv;
+    s.Ft = mu.fiso * fse;
+    s.Fa = mu.fiso * a * fal * fvv;
+    s.Ff = mu.fiso * (a * fal * fvv + fpe + mu.beta * vN);
+    s.clamped = clamped;
+    Real dGdl = (a * dfal * fvv + dfpe) * mu.inv_lopt + dfse * mu.inv_lts / (cosphi * cosphi) + fse * w * w / (sq * sq * sq);
+    s.dvdl = clamped ? Real(0) : -(dGdl / dGdv) * mu.lv;
+    Real u = excitation < mu.amin ? mu.amin : (excitation > Real(1) ? Real(1) : excitation);
+    Real tau = u > a ? mu.tau_act * (Real(0.5) + Real(1.5) * a) : mu.tau_deact / (Real(0.5) + Real(1.5) * a);
+    s.dadt = (u - a) / tau;
+}
+
+/* static fiber equilibrium at reset (zero fiber velocity) */
+template <typename Real>
+DEV Real muscle_equilibrium(const DMuscle<Real> &mu, Real a_state, Real L) {
+    Real a = a_state < mu.amin ? mu.amin : (a_state > Real(1) ? Real(1) : a_state);
+    Real w = mu.width, lo = mu.lmin;
+    Real hi = sqrt((L - mu.lts) * (L - mu.lts) + w * w);
+    if (!(L - mu.lts > sqrt(lo * lo - w * w))) return lo;
+    {   /* the fiber out-pulls the tendon even at its minimum length: no root */
+        Real sq = sqrt(lo * lo - w * w), fal, dfal, fpe, dfpe, fse, dfse;
+        curve_eval(mu.fal, lo * mu.inv_lopt, fal, dfal);
+        curve_eval(mu.fpe, lo * mu.inv_lopt, fpe, dfpe);
+        curve_eval(mu.fse, (L - sq) * mu.inv_lts, fse, dfse);
+        if ((a * fal + fpe) * (sq / lo) - fse >= 0) return lo;
+    }
+    Real l = sqrt((L - Real(1.01) * mu.lts) * (L - Real(1.01) * mu.lts) + w * w);
+    if (!(l > lo && l < hi)) l = Real(0.5) * (lo + hi);
+    for (int it = 0; it < 4 * Eps<Real>::it_max; ++it) {
+        Real sq = sqrt(l * l - w * w), cphi = sq / l;
+        Real fal, dfal, fpe, dfpe, fse, dfse;
+        curve_eval(mu.fal, l * mu.inv_lopt, fal, dfal);
+        curve_eval(mu.fpe, l * mu.inv_lopt, fpe, dfpe);
+        curve_eval(mu.fse, (L - sq) * mu.inv_lts, fse, dfse);
+        Real H = (a * fal + fpe) * cphi - fse;
+        Real dH = (a * dfal + dfpe) * mu.inv_lopt * cphi + (a * fal + fpe) * (w * w) / (l * l * sq) + dfse * mu.inv_lts / cphi;
+        if (H > 0) hi = l; else lo = l;
+        Real ln = l - H / dH;
+        if (!(ln > lo && ln < hi)) ln = Real(0.5) * (lo + hi);
+        Real dl = ln - l;
+        l = ln;
+        if (fabs(dl) <= Eps<Real>::l_tol) break;
+    }
+    return l;
+}
+
+/* path length, moment arms dL/dq for the muscle of this lane (body frames
+ * and coordinates from LDS, Plucker columns from registers) */
+template <class T, typename Real>
+DEV void muscle_path(const DModel<Real> &M, const Work<T, Real> &W, const Real *ldsR, const Real *ldsq, int m,
+                     Real &L, Real *dLdq) {
+    const DMuscle<Real> &mu = M.mus[m];
+    L = 0;
+#pragma unroll
+    for (int d = 0; d < T::ND; ++d) dLdq[d] = 0;
+    Real Pp[3] = {0, 0, 0}, ep[3] = {0, 0, 0}, dPp[3] = {0, 0, 0};
+    uint32_t maskp = 0;
+    int mdofp = -1;
+    bool have = false;
+    for (int j = 0; j < mu.npt; ++j) {
+        const DPathPt<Real> &pt = M.pt[mu.pt_off + j];
+        if (pt.type == BIOIM_PT_COND) {
+            Real qc = ldsq[pt.cond_coord];
+            if (qc < pt.lo || qc > pt.hi) continue;
+        }
+        Real loc[3], dloc[3] = {0, 0, 0};
+        if (pt.type == BIOIM_PT_MOVING) {
+            Real ll[3], dl[3] = {0, 0, 0};
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                if (pt.fn[a] < 0) { ll[a] = pt.loc[a]; continue; }
+                Real f, f1, f2;
+                fn_eval_rt(M, pt.fn[a], ldsq[pt.mcoord], f, f1, f2);
+                ll[a] = f; dl[a] = f1;
+            }
+            mv3(pt.R, ll, loc);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) loc[i] += pt.p[i];
+            mv3(pt.R, dl, dloc);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) loc[i] = pt.loc[i];
+        }
+        const Real *Rb = ldsR + 12 * pt.cbody;
+        Real P[3], dP[3];
+        mv3(Rb, loc, P);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) P[i] += Rb[9 + i];
+        mv3(Rb, dloc, dP);
+        Real e[3] = {0, 0, 0};
+        if (have) {
+            Real sgm[3] = {P[0] - Pp[0], P[1] - Pp[1], P[2] - Pp[2]};
+            Real len = sqrt(dot3(sgm, sgm));
+            L += len;
+            Real inv = Real(1) / len;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) e[a] = sgm[a] * inv;
+            /* previous point is now complete: g = e_prev_prev - e */
+            Real g[3] = {ep[0] - e[0], ep[1] - e[1], ep[2] - e[2]}, mo[3];
+            cross3(Pp, g, mo);
+            sfor<0, T::ND>([&](auto dI) {
+                constexpr int d = decltype(dI)::value;
+                Real on = (maskp >> d) & 1u ? Real(1) : Real(0);
+                dLdq[d] += on * (dot3(W.S[d], mo) + dot3(W.S[d] + 3, g)) + (mdofp == d ? dot3(g, dPp) : Real(0));
+            });
+        }
+#pragma unroll
+        for (int a = 0; a < 3; ++a) { ep[a] = e[a]; Pp[a] = P[a]; dPp[a] = dP[a]; }
+        maskp = pt.dofmask;
+        mdofp = pt.mdof;
+        have = true;
+    }
+    if (have) { /* last point: g = e_prev */
+        Real g[3] = {ep[0], ep[1], ep[2]}, mo[3];
+        cross3(Pp, g, mo);
+        sfor<0, T::ND>([&](auto dI) {
+            constexpr int d = decltype(dI)::value;
+            Real on = (maskp >> d) & 1u ? Real(1) : Real(0);
+            dLdq[d] += on * (dot3(W.S[d], mo) + dot3(W.S[d] + 3, g)) + (mdofp == d ? dot3(g, dPp) : Real(0));
+        });
+    }
+}
+
+/* -------------------------------------------------------- env context */
+template <class T, typename Real> struct Lds {
+    static constexpr int BODY = 12 * T::NB;     /* R, o per composite */
+    static constexpr int Q = BODY;              /* qf[NC]             */
+    static constexpr int OBS = ((Q + T::NC + 3) / 4) * 4;
+    static constexpr int SIZE = OBS + BIOIM_OBS_MAX;
+};
+
+template <class T, typename Real> struct Dyn {
+    Real qdd[T::ND];
+    MState<Real> ms;             /* this lane's muscle */
+    Contact<T, Real> co;
+    Real limf[T::NL > 0 ? T::NL : 1];
+    bool ok;
+};
+
+/* full dynamics at (q, u, lane muscle state) with controls; h > 0 gives the
+ * implicit-step increment, h == 0 the true accelerations */
+template <class T, typename Real>
+DEV void dynamics(const DModel<Real> &M, Work<T, Real> &W, const Real *q, const Real *u, Real act, Real lce,
+                  Real control, int lane, Real *lds, Real h, Dyn<T, Real> &D) {
+    constexpr int ND = T::ND;
+    fill_coords<T, Real>(M, q, u, W);
+    kinematics<T, Real>(M, W);
+    if constexpr (T::NM > 0) {
+        /* stage composite frames + coordinates for the muscle lanes */
+        if (lane == 0) {
+            sfor<0, T::NB>([&](auto cI) {
+                constexpr int c = decltype(cI)::value;
+#pragma unroll
+                for (int i = 0; i < 9; ++i) lds[12 * c + i] = W.K[c].R[i];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) lds[12 * c + 9 + i] = W.K[c].o[i];
+            });
+#pragma unroll
+            for (int c = 0; c < T::NC; ++c) lds[Lds<T, Real>::Q + c] = W.qf[c];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    Real Mp[Work<T, Real>::NP], bias[ND], tau[ND];
+    mass_bias<T, Real>(M, W, Mp, bias);
+#pragma unroll
+    for (int d = 0; d < ND; ++d) tau[d] = 0;
+    if constexpr (T::NM > 0) {
+        Real dLdq[ND];
+        Real L = 0;
+        if (lane < T::NM) {
+            muscle_path<T, Real>(M, W, lds, lds + Lds<T, Real>::Q, lane, L, dLdq);
+            muscle_eval(M.mus[lane], act, lce, control, L, D.ms);
+#pragma unroll
+            for (int d = 0; d < ND; ++d) tau[d] = -D.ms.Ft * dLdq[d];
+        }
+#pragma unroll
+        for (int d = 0; d < ND; ++d) tau[d] = group_sum<T::G>(tau[d]);
+        __builtin_amdgcn_wave_barrier();
+    } else {
+        /* coordinate actuators: action entry i acts on dof act_dof[i] */
+        sfor<0, T::NA>([&](auto iI) {
+            constexpr int i = decltype(iI)::value;
+            constexpr int d = T::act_dof[i];
+            if constexpr (d >= 0) {
+                Real ci = __shfl(control, ((threadIdx.x & 63) & ~(T::G - 1)) + i, 64);
+                tau[d] += ci * M.ca_opt[i];
+            }
+        });
+    }
+    Real *Meff = Mp;
+    contact_all<T, Real>(M, W, tau, Meff, h, D.co);
+    sfor<0, T::NL>([&](auto lI) {
+        constexpr int l = decltype(lI)::value;
+        constexpr int d = T::limit_dof[l];
+        constexpr int cc = T::limit_coord[l];
+        Real qv = W.qf[cc], qd = W.uf[cc];
+        Real qup = M.lim_qup[l], qlo = M.lim_qlow[l], tr = M.lim_trans[l];
+        Real up = smooth_step(Real(0), Real(1), qup, qup + tr, qv);
+        Real lo = smooth_step(Real(1), Real(0), qlo - tr, qlo, qv);
+        Real f = -M.lim_kup[l] * up * (qv - qup) + M.lim_klow[l] * lo * (qlo - qv) - M.lim_damp[l] * (up + lo) * qd;
+        D.limf[l] = f;
+        if constexpr (d >= 0) {
+            tau[d] += f;
+            if (h > 0) {
+                Real dup = smooth_step_d(Real(0), Real(1), qup, qup + tr, qv);
+                Real dlo = smooth_step_d(Real(1), Real(0), qlo - tr, qlo, qv);
+                Real kq = M.lim_kup[l] * (up + dup * (qv - qup)) + M.lim_klow[l] * (lo - dlo * (qlo - qv));
+                Real cq = M.lim_damp[l] * (up + lo);
+                Meff[tri<0>(d, d)] += h * cq + h * h * kq;
+                tau[d] -= h * kq * qd;
+            }
+        }
+    });
+#pragma unroll
+    for (int d = 0; d < ND; ++d) D.qdd[d] = tau[d] - bias[d];
+    D.ok = cholesky_solve<ND, Real>(Meff, D.qdd);
+}
+
+/* body origin (OpenSim body ob) / system COM (ob = -1) */
+template <class T, int OB, typename Real>
+DEV void report_body(const DModel<Real> &M, const Work<T, Real> &W, Real *pos, Real *vel) {
+    if constexpr (OB >= 0) {
+        constexpr int c = T::os_cb[OB];
+        const Kin<Real> &k = W.K[c];
+        mv3(k.R, M.os_p[OB], pos);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) pos[i] += k.o[i];
+        point_vel(k, pos, vel);
+    } else {
+        Real mt = 0, cs[3] = {0, 0, 0}, vs[3] = {0, 0, 0};
+        sfor<0, T::NB>([&](auto cI) {
+            constexpr int c = decltype(cI)::value;
+            const Kin<Real> &k = W.K[c];
+            Real cG[3], vc[3];
+            mv3(k.R, M.com[c], cG);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) cG[i] += k.o[i];
+            point_vel(k, cG, vc);
+            Real m = M.mass[c];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { cs[i] += m * cG[i]; vs[i] += m * vc[i]; }
+            mt += m;
+        });
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { pos[i] = cs[i] / mt; vel[i] = vs[i] / mt; }
+    }
+}
+
+template <int N> DEV int clamp_row(int r, int nrows) { return r < 0 ? 0 : (r >= nrows ? nrows - 1 : r); }
+
+/* counter-based RNG (splitmix64) for device-drawn reset indices */
+DEV uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+DEV int draw_index(uint64_t seed, int env, int count, int hi) {
+    uint64_t r = splitmix64(seed ^ splitmix64(((uint64_t)env << 32) | (uint32_t)count));
+    return (int)(r % (uint64_t)(hi + 1));
+}
+
+/* ---------------------------------------------------------------- kernel
+ * mode 0: env step (optionally auto-reset); mode 1: reset listed envs */
+template <class T, typename Real>
+__global__ __launch_bounds__(256) void env_kernel(const DModel<Real> *__restrict__ Mg, DState<Real> st, int N, int mode,
+                                                  const Real *__restrict__ actions, Real *__restrict__ obs,
+                                                  Real *__restrict__ reward, uint8_t *__restrict__ done_out,
+                                                  Real *__restrict__ info, const int32_t *__restrict__ env_ids,
+                                                  const int32_t *__restrict__ ref_index, int n_list, int auto_reset,
+                                                  uint64_t seed) {
+    constexpr int G = T::G, ND = T::ND, NA = T::NA, NM = T::NM;
+    constexpr int ENVS_PER_BLOCK = 256 / G;
+    extern __shared__ __align__(16) unsigned char smem_raw[];
+    Real *smem = reinterpret_cast<Real *>(smem_raw);
+    const DModel<Real> &M = *Mg;
+    const int lane = threadIdx.x % G;
+    const int slot = threadIdx.x / G;
+    int gidx = blockIdx.x * ENVS_PER_BLOCK + slot;
+    Real *lds = smem + slot * Lds<T, Real>::SIZE;
+    int env;
+    if (mode == 1) {
+        if (gidx >= n_list) return;
+        env = env_ids ? env_ids[gidx] : gidx;
+        if (env < 0 || env >= N) return;
+    } else {
+        if (gidx >= N) return;
+        env = gidx;
+    }
+    const int H = M.horizon;
+    Work<T, Real> W;
+    Dyn<T, Real> D;
+    Real q[ND], u[ND];
+#pragma unroll
+    for (int d = 0; d < ND; ++d) { q[d] = st.q[(size_t)d * N + env]; u[d] = st.u[(size_t)d * N + env]; }
+    double t = st.t[env];
+    int istep = st.istep[env], has_last = st.has_last[env], resets = st.resets[env];
+    Real old_px = st.old_px[env];
+    Real act = 0, lce = 0, control = 0, curr = 0, last = 0, hist[BIOIM_MAX_HORIZON];
+    if (NM > 0 && lane < NM) { act = st.act[(size_t)lane * N + env]; lce = st.lce[(size_t)lane * N + env]; }
+    if (lane < NA) {
+        last = st.last[(size_t)lane * N + env];
+        for (int hh = 0; hh < H; ++hh) hist[hh] = st.hist[((size_t)hh * NA + lane) * N + env];
+    }
+    int done = 0;
+    Real rew = 0, inf[5] = {0, 0, 0, 0, 0};
+    bool do_reset = (mode == 1);
+    int reset_row = 0;
+    if (mode == 1) reset_row = ref_index ? ref_index[gidx] : draw_index(seed, env, resets, M.reset_hi);
+
+    if (mode == 0) {
+        /* ---- action pre-processing (Env.step) */
+        Real raw = lane < NA ? actions[(size_t)env * NA + lane] : Real(0);
+        bool anynan = group_any<G>(lane < NA && isnan(raw));
+        Real a = anynan ? Real(0) : raw;
+        if constexpr ((T::FLAGS & BIOIM_ENV_PD) != 0) {
+            if (!anynan) {
+                fill_coords<T, Real>(M, q, u, W);
+                Real xq = 0, xu = 0;
+                sfor<0, NA>([&](auto iI) {
+                    constexpr int i = decltype(iI)::value;
+                    if (lane == i) { xq = W.qf[T::pd_coord[i]]; xu = W.uf[T::pd_coord[i]]; }
+                });
+                if (lane < NA) a = M.kp[lane] * (raw - xq) - M.kv[lane] * xu;
+            }
+        }
+        if (!has_last) {
+            last = a;
+            for (int hh = 0; hh < H; ++hh) hist[hh] = a;
+        }
+        has_last = 1;
+        for (int hh = 0; hh + 1 < H; ++hh) hist[hh] = hist[hh + 1];
+        hist[H - 1] = a;
+        Real s = 0;
+        for (int hh = 0; hh < H; ++hh) s += hist[hh];
+        curr = s / Real(H);
+        Real phys = (T::FLAGS & BIOIM_ENV_RAW_ACTION) ? a : curr;
+        bool pnan = group_any<G>(lane < NA && isnan(phys));
+        Real lo = NM > 0 ? Real(0) : M.ca_min[lane < NA ? lane : 0];
+        Real hi = NM > 0 ? Real(1) : M.ca_max[lane < NA ? lane : 0];
+        Real v = pnan ? Real(0) : phys;
+        control = lane < NA ? (v < lo ? lo : (v > hi ? hi : v)) : Real(0);
+        /* ---- integrate to step_size * istep */
+        istep += 1;
+        double tf = M.step_size * (double)istep;
+        double hstep = tf - t;
+        if (hstep > 0) {
+            Real dt = Real(hstep / (double)M.nsub);
+            for (int s_ = 0; s_ < M.nsub; ++s_) {
+                dynamics<T, Real>(M, W, q, u, act, lce, control, lane, lds, dt, D);
+#pragma unroll
+                for (int d = 0; d < ND; ++d) { u[d] += dt * D.qdd[d]; q[d] += dt * u[d]; }
+                if (NM > 0 && lane < NM) {
+                    act += dt * D.ms.dadt;
+                    if (!D.ms.clamped) {
+                        Real ln = lce + dt * D.ms.vce / (Real(1) - dt * D.ms.dvdl);
+                        lce = ln < M.mus[lane].lmin ? M.mus[lane].lmin : ln;
+                    }
+                }
+            }
+        }
+        t = tf;
+    }
+
+    for (int pass = 0; pass < 2; ++pass) {
+        if (pass == 1 || do_reset) {
+            if (!do_reset) break;
+            /* ---- reset to reference row (Env.reset) */
+            int r = clamp_row<0>(reset_row, M.nrows);
+            sfor<0, T::NC>([&](auto cI) {
+                constexpr int c = decltype(cI)::value;
+                constexpr int d = T::coord_dof[c];
+                if constexpr (d >= 0) { q[d] = M.ref_q[r][c]; u[d] = M.ref_u[r][c]; }
+            });
+            t = M.ref_time[r];
+            istep = M.ref_istep[r];
+            has_last = 0;
+            control = 0;
+            resets += 1;
+            if constexpr (NM > 0) {
+                fill_coords<T, Real>(M, q, u, W);
+                kinematics<T, Real>(M, W);
+                if (lane == 0) {
+                    sfor<0, T::NB>([&](auto cI) {
+                        constexpr int c = decltype(cI)::value;
+#pragma unroll
+                        for (int i = 0; i < 9; ++i) lds[12 * c + i] = W.K[c].R[i];
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) lds[12 * c + 9 + i] = W.K[c].o[i];
+                    });
+#pragma unroll
+                    for (int c = 0; c < T::NC; ++c) lds[Lds<T, Real>::Q + c] = W.qf[c];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (lane < NM) {
+                    Real L, dLdq[ND];
+                    muscle_path<T, Real>(M, W, lds, lds + Lds<T, Real>::Q, lane, L, dLdq);
+                    act = M.mus[lane].default_act;
+                    lce = muscle_equilibrium(M.mus[lane], act, L);
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        /* ---- realize at the current state */
+        dynamics<T, Real>(M, W, q, u, act, lce, control, lane, lds, Real(0), D);
+        Real *ob = lds + Lds<T, Real>::OBS;
+        const bool tgt = (M.env_flags & BIOIM_ENV_TARGET_OBS) != 0, grf = (M.env_flags & BIOIM_ENV_GRF_OBS) != 0;
+        Real qdd_f[T::NC];
+        sfor<0, T::NC>([&](auto cI) {
+            constexpr int c = decltype(cI)::value;
+            constexpr int d = T::coord_dof[c];
+            if constexpr (d >= 0) qdd_f[c] = D.qdd[d]; else qdd_f[c] = 0;
+        });
+        Real px = W.qf[T::TX], py = W.qf[T::TY];
+        Real pz = 0;
+        if constexpr (T::TZ >= 0) pz = W.qf[T::TZ];
+        /* observation (get_state_dict + flatten), staged in LDS */
+        if (lane == 0) {
+            int k = 0;
+            double ph = (double)istep / (double)M.cycle;
+            ob[k++] = Real(ph - floor(ph));
+            sfor<0, T::NC>([&](auto cI) {
+                constexpr int c = decltype(cI)::value;
+                if constexpr (c != T::TX && c != T::TY && c != T::TZ) ob[k++] = W.qf[c];
+            });
+#pragma unroll
+            for (int c = 0; c < T::NC; ++c) ob[k++] = W.uf[c];
+#pragma unroll
+            for (int c = 0; c < T::NC; ++c) ob[k++] = qdd_f[c];
+            if (tgt) {
+                int r = clamp_row<0>(istep + 1, M.nrows);
+#pragma unroll
+                for (int c = 0; c < T::NC; ++c)
+                    if (c != T::TX) ob[k++] = M.ref_q[r][c];
+#pragma unroll
+                for (int c = 0; c < T::NC; ++c)
+                    if (c != T::TX) ob[k++] = M.ref_u[r][c];
+            }
+            sfor<0, T::NOBP>([&](auto bI) {
+                constexpr int b = decltype(bI)::value;
+                Real p3[3], v3[3];
+                report_body<T, T::obs_bpos[b], Real>(M, W, p3, v3);
+                ob[k++] = p3[0] - px; ob[k++] = p3[1] - py; ob[k++] = p3[2] - pz;
+            });
+            sfor<0, T::NOBV>([&](auto bI) {
+                constexpr int b = decltype(bI)::value;
+                Real p3[3], v3[3];
+                report_body<T, T::obs_bvel[b], Real>(M, W, p3, v3);
+                ob[k++] = v3[0]; ob[k++] = v3[1]; ob[k++] = v3[2];
+            });
+            k += 3 * NM;
+            if (grf) {
+                sfor<0, T::NF>([&](auto fI) {
+                    constexpr int f = decltype(fI)::value;
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) ob[k++] = D.co.F[f][i] / M.weight;
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) ob[k++] = D.co.Mo[f][i] / M.moment;
+                });
+            }
+        }
+        if constexpr (NM > 0) {
+            int mb = 1 + (T::NC - (T::TX >= 0) - (T::TY >= 0) - (T::TZ >= 0)) + 2 * T::NC +
+                     (tgt ? 2 * (T::NC - 1) : 0) + 3 * T::NOBP + 3 * T::NOBV;
+            if (lane < NM) {
+                ob[mb + 3 * lane] = D.ms.act;
+                ob[mb + 3 * lane + 1] = D.ms.lce;
+                ob[mb + 3 * lane + 2] = D.ms.vce;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (obs)
+            for (int k = lane; k < M.obs_dim; k += G) obs[(size_t)env * M.obs_dim + k] = ob[k];
+        __builtin_amdgcn_wave_barrier();
+        if (pass == 1 || mode == 1) break;
+
+        /* ---- reward (get_reward) and termination (is_done) */
+        {
+            int r = clamp_row<0>(istep, M.nrows);
+            Real qerr = 0;
+#pragma unroll
+            for (int c = 0; c < T::NC; ++c) {
+                Real e = W.qf[c] - M.ref_q[r][c];
+                qerr += e * e;
+            }
+            qerr /= Real(T::NC);
+            Real err[BIOIM_NREFBODY];
+            sfor<0, BIOIM_NREFBODY>([&](auto bI) {
+                constexpr int b = decltype(bI)::value;
+                Real p3[3], v3[3];
+                report_body<T, T::rw_body[b], Real>(M, W, p3, v3);
+                Real s = 0;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    Real e = p3[i] - M.ref_x[r][b][i];
+                    s += e * e;
+                }
+                err[b] = s / Real(3);
+            });
+            Real position_r = exp(Real(-30) * qerr);
+            Real com_r = exp(Real(-20) * err[0]);
+            Real foot_r = Real(0.5) * exp(Real(-20) * (err[7] + err[1] + err[3] + err[5]));
+            Real foot_l = Real(0.5) * exp(Real(-20) * (err[8] + err[2] + err[4] + err[6]));
+            Real pelvis_x = px;
+            Real da = lane < NA ? curr - last : Real(0);
+            Real action_r = exp(-M.action_r_scale * sqrt(group_sum<G>(da * da)));
+            Real effort, a_error = 0;
+            if constexpr (NM > 0) {
+                Real an = lane < NM ? D.ms.act * D.ms.act : Real(0);
+                a_error = exp(Real(-2) * sqrt(group_sum<G>(an)));
+                Real cot = 0;
+                if (lane < NM) {
+                    const DMuscle<Real> &mu = M.mus[lane];
+                    Real l = mu.slow, ex = control, aa = D.ms.act, hp = Real(0.5 * 3.14159265358979323846);
+                    Real fa = Real(40) * l * sin(hp * ex) + Real(133) * (Real(1) - l) * (Real(1) - cos(hp * ex));
+                    Real fm = Real(74) * l * sin(hp * aa) + Real(111) * (Real(1) - l) * (Real(1) - cos(hp * aa));
+                    Real ln = D.ms.lce * mu.inv_lopt, vv = D.ms.vce;
+                    Real g = 0;
+                    if (ln < Real(0.5)) g = Real(0.5);
+                    else if (ln < Real(1)) g = ln;
+                    else if (ln < Real(1.5)) g = Real(-2) * ln + Real(3);
+                    Real es = fmax(Real(0), Real(0.25) * D.ms.Ff * -vv);
+                    Real ew = fmax(Real(0), D.ms.Fa * -vv);
+                    cot = mu.mass * fa + mu.mass * g * fm + es + ew;
+                }
+                cot = group_sum<G>(cot) + Real(1.51) * M.total_mass;
+                effort = cot / (Real(20) * Real(NM * NM));
+            } else {
+                Real cn = lane < NA ? curr * curr : Real(0);
+                effort = sqrt(group_sum<G>(cn)) / (M.max_actuation * Real(NA * NA));
+            }
+            Real effort_r = exp(-effort / fmax(pelvis_x - old_px + Real(1), Real(1)));
+            Real imit = position_r * com_r;
+            if constexpr ((T::FLAGS & BIOIM_ENV_REWARD_FEET) != 0) imit *= (foot_l + foot_r);
+            rew = (Real(0.5) + M.w_imitate) * imit + M.w_effort * effort_r + M.w_action * action_r;
+            inf[0] = position_r; inf[1] = com_r; inf[2] = foot_l; inf[3] = foot_r; inf[4] = a_error;
+            last = curr;
+            old_px = pelvis_x;
+            /* is_done */
+            Real p3[3], v3[3];
+            report_body<T, T::TORSO, Real>(M, W, p3, v3);
+            Real lmax = 0, amax = 0;
+            sfor<0, T::NL>([&](auto lI) { lmax = fmax(lmax, fabs(D.limf[decltype(lI)::value])); });
+#pragma unroll
+            for (int c = 0; c < T::NC; ++c)
+                if (T::coord_dof[c] >= 0) amax = fmax(amax, fabs(qdd_f[c]));
+            int d_ = 0;
+            if (p3[1] < M.torso_y_min) d_ = 1;
+            else if (lmax > M.limit_force_max) d_ = 1;
+            else if (amax > M.acc_max) d_ = 1;
+            else if (istep >= M.n_episode) d_ = 1;
+            else if constexpr ((T::FLAGS & BIOIM_ENV_DONE_CROSS) != 0) {
+                Real pr[3], pl[3];
+                report_body<T, T::CALCN_R, Real>(M, W, pr, v3);
+                report_body<T, T::CALCN_L, Real>(M, W, pl, v3);
+                if (pr[2] - pl[2] < 0) d_ = 1;
+            }
+#pragma unroll
+            for (int d = 0; d < ND; ++d)
+                if (!isfinite(q[d]) || !isfinite(u[d])) d_ = 1;
+            if (!D.ok) d_ = 1;
+            done = d_;
+        }
+        if (lane == 0) {
+            if (reward) reward[env] = rew;
+            done_out[env] = (uint8_t)done;
+        }
+        if (info && lane < M.info_dim) {
+            Real iv = inf[0];
+#pragma unroll
+            for (int i = 1; i < 5; ++i) iv = lane == i ? inf[i] : iv;
+            info[(size_t)env * M.info_dim + lane] = iv;
+        }
+        if (done && auto_reset) {
+            do_reset = true;
+            reset_row = draw_index(seed, env, resets, M.reset_hi);
+        } else {
+            break;
+        }
+    }
+
+    /* ---- store state */
+    if (lane == 0) {
+        st.t[env] = t;
+        st.istep[env] = istep;
+        st.has_last[env] = has_last;
+        st.old_px[env] = old_px;
+        st.done[env] = (mode == 0 && !do_reset) ? done : 0;
+        st.resets[env] = resets;
+    }
+    if (lane < ND) {
+        Real qv = q[0], uv = u[0];
+#pragma unroll
+        for (int d = 1; d < ND; ++d) { qv = lane == d ? q[d] : qv; uv = lane == d ? u[d] : uv; }
+        st.q[(size_t)lane * N + env] = qv;
+        st.u[(size_t)lane * N + env] = uv;
+    }
+    if (NM > 0 && lane < NM) { st.act[(size_t)lane * N + env] = act; st.lce[(size_t)lane * N + env] = lce; }
+    if (lane < NA) {
+        st.last[(size_t)lane * N + env] = last;
+        for (int hh = 0; hh < H; ++hh) st.hist[((size_t)hh * NA + lane) * N + env] = hist[hh];
+    }
+}
+
+/* =================================================================== host */
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(x)                                                                       \
+    do {                                                                                \
+        hipError_t e_ = (x);                                                            \
+        if (e_ != hipSuccess) return fail(BIOIM_E_DEVICE, std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+template <typename Real> void convert_curve(const bioim_curve_t &s, DCurve<Real> &d) {
+    for (int i = 0; i < BIOIM_MAX_CURVESEG; ++i)
+        for (int j = 0; j < 6; ++j) { d.x[i][j] = (Real)s.x[i][j]; d.y[i][j] = (Real)s.y[i][j]; }
+    d.x0 = (Real)s.x0; d.y0 = (Real)s.y0; d.dydx0 = (Real)s.dydx0;
+    d.x1 = (Real)s.x1; d.y1 = (Real)s.y1; d.dydx1 = (Real)s.dydx1;
+    d.nseg = s.nseg;
+}
+
+template <typename Real> void convert_model(const bioim_modelpack_t &p, DModel<Real> &m, const std::vector<uint32_t> &dofmask) {
+    memset(&m, 0, sizeof(m));
+    for (int c = 0; c < p.ncbody; ++c) {
+        const bioim_cbody_t &b = p.cbody[c];
+        for (int i = 0; i < 9; ++i) { m.R_pf[c][i] = (Real)b.R_pf[i]; m.R_mb[c][i] = (Real)b.R_mb[i]; }
+        for (int i = 0; i < 3; ++i) { m.p_pf[c][i] = (Real)b.p_pf[i]; m.p_mb[c][i] = (Real)b.p_mb[i]; m.com[c][i] = (Real)b.com[i]; }
+        for (int a = 0; a < 6; ++a) {
+            m.fn[c][a] = b.fn[a];
+            for (int i = 0; i < 3; ++i) m.axis[c][a][i] = (Real)b.axis[a][i];
+        }
+        m.mass[c] = (Real)b.mass;
+        for (int i = 0; i < 6; ++i) m.inertia[c][i] = (Real)b.inertia[i];
+    }
+    for (int f = 0; f < p.nfn; ++f) {
+        m.fn_type[f] = p.fn[f].type; m.fn_coord[f] = p.fn[f].coord; m.fn_off[f] = p.fn[f].knot_off;
+        m.fn_n[f] = p.fn[f].nknots; m.fn_a[f] = (Real)p.fn[f].a; m.fn_b[f] = (Real)p.fn[f].b;
+    }
+    for (int k = 0; k < p.nknots; ++k) {
+        m.kx[k] = (Real)p.knot_x[k]; m.ky[k] = (Real)p.knot_y[k]; m.kb[k] = (Real)p.knot_b[k];
+        m.kc[k] = (Real)p.knot_c[k]; m.kd[k] = (Real)p.knot_d[k];
+    }
+    for (int c = 0; c < p.ncoord; ++c) { m.coord_default[c] = (Real)p.coord[c].default_value; m.coord_dof[c] = p.coord[c].dof; }
+    for (int b = 0; b < p.nosbody; ++b) {
+        for (int i = 0; i < 9; ++i) m.os_R[b][i] = (Real)p.osbody[b].R[i];
+        for (int i = 0; i < 3; ++i) m.os_p[b][i] = (Real)p.osbody[b].p[i];
+    }
+    for (int i = 0; i < p.nmuscle; ++i) {
+        const bioim_muscle_t &s = p.muscle[i];
+        DMuscle<Real> &d = m.mus[i];
+        d.fiso = (Real)s.fiso; d.lopt = (Real)s.lopt; d.inv_lopt = (Real)(1.0 / s.lopt);
+        d.lts = (Real)s.lts; d.inv_lts = (Real)(1.0 / s.lts); d.lv = (Real)(s.lopt * s.vmax);
+        d.tau_act = (Real)s.tau_act; d.tau_deact = (Real)s.tau_deact; d.amin = (Real)s.amin; d.beta = (Real)s.damping;
+        d.width = (Real)s.width; d.lmin = (Real)s.lmin; d.slow = (Real)s.slow_twitch; d.mass = (Real)s.mass;
+        d.default_act = (Real)s.default_act; d.pt_off = s.pt_off; d.npt = s.npt;
+        convert_curve(s.fal, d.fal); convert_curve(s.fv, d.fv); convert_curve(s.fpe, d.fpe); convert_curve(s.fse, d.fse);
+    }
+    for (int j = 0; j < p.npathpt; ++j) {
+        const bioim_pathpt_t &s = p.pathpt[j];
+        DPathPt<Real> &d = m.pt[j];
+        d.type = s.type; d.cbody = s.cbody; d.cond_coord = s.cond_coord;
+        d.mcoord = -1; d.mdof = -1;
+        for (int a = 0; a < 3; ++a) {
+            d.fn[a] = s.fn[a];
+            if (s.type == BIOIM_PT_MOVING && s.fn[a] >= 0) {
+                d.mcoord = p.fn[s.fn[a]].coord;
+                d.mdof = d.mcoord >= 0 ? p.coord[d.mcoord].dof : -1;
+            }
+        }
+        d.dofmask = dofmask[s.cbody];
+        for (int i = 0; i < 3; ++i) { d.loc[i] = (Real)s.loc[i]; d.p[i] = (Real)s.p[i]; }
+        for (int i = 0; i < 9; ++i) d.R[i] = (Real)s.R[i];
+        d.lo = (Real)s.range_lo; d.hi = (Real)s.range_hi;
+    }
+    for (int s = 0; s < p.nsphere; ++s) {
+        for (int i = 0; i < 3; ++i) m.sph_loc[s][i] = (Real)p.sphere[s].loc[i];
+        m.sph_r[s] = (Real)p.sphere[s].radius;
+    }
+    for (int f = 0; f < p.ncforce; ++f) {
+        const bioim_cforce_t &c = p.cforce[f];
+        m.cf_kk[f] = (Real)(0.5 * pow(c.stiffness, 2.0 / 3.0));
+        m.cf_c[f] = (Real)c.dissipation; m.cf_ms[f] = (Real)c.static_friction; m.cf_md[f] = (Real)c.dynamic_friction;
+        m.cf_mv[f] = (Real)c.viscous_friction; m.cf_vt[f] = (Real)c.transition_velocity;
+    }
+    for (int l = 0; l < p.nlimit; ++l) {
+        const bioim_limit_t &s = p.limit[l];
+        m.lim_qup[l] = (Real)s.qup; m.lim_qlow[l] = (Real)s.qlow; m.lim_kup[l] = (Real)s.kup;
+        m.lim_klow[l] = (Real)s.klow; m.lim_damp[l] = (Real)s.damping; m.lim_trans[l] = (Real)s.trans;
+    }
+    for (int a = 0; a < p.ncoordact; ++a) {
+        m.ca_opt[a] = (Real)p.coordact[a].optimal_force;
+        m.ca_min[a] = (Real)p.coordact[a].min_control;
+        m.ca_max[a] = (Real)p.coordact[a].max_control;
+    }
+    for (int a = 0; a < BIOIM_MAX_ACT; ++a) { m.kp[a] = (Real)p.kp[a]; m.kv[a] = (Real)p.kv[a]; }
+    m.w_imitate = (Real)p.w_imitate; m.w_effort = (Real)p.w_effort; m.w_action = (Real)p.w_action;
+    m.action_r_scale = (Real)p.action_r_scale; m.max_actuation = (Real)p.max_actuation;
+    m.total_mass = (Real)p.total_mass;
+    double wgt = fabs(p.total_mass * p.gravity[1]);
+    m.weight = (Real)wgt;
+    m.moment = (Real)(wgt * p.height);
+    m.torso_y_min = (Real)p.torso_y_min; m.limit_force_max = (Real)p.limit_force_max; m.acc_max = (Real)p.acc_max;
+    for (int i = 0; i < 3; ++i) m.gravity[i] = (Real)p.gravity[i];
+    m.horizon = p.horizon; m.cycle = p.cycle; m.n_episode = p.n_episode; m.reset_hi = p.reset_hi;
+    m.nsub = p.nsub; m.nrows = p.nrows; m.obs_dim = p.obs_dim; m.info_dim = p.info_dim; m.env_flags = p.env_flags;
+    m.step_size = p.step_size;
+    for (int r = 0; r < p.nrows; ++r) {
+        m.ref_time[r] = p.ref_time[r];
+        m.ref_istep[r] = p.ref_istep[r];
+        for (int c = 0; c < p.ncoord; ++c) { m.ref_q[r][c] = (Real)p.ref_q[r][c]; m.ref_u[r][c] = (Real)p.ref_u[r][c]; }
+        for (int b = 0; b < BIOIM_NREFBODY; ++b)
+            for (int i = 0; i < 3; ++i) m.ref_x[r][b][i] = (Real)p.ref_x[r][b][i];
+    }
+}
+
+/* structural match of a pack against a compiled topology */
+template <class T> bool topology_matches(const bioim_modelpack_t &p, std::vector<uint32_t> &dofmask) {
+    if (p.ncbody != T::NB || p.ndof != T::ND || p.ncoord != T::NC || p.nmuscle != T::NM || p.nact != T::NA ||
+        p.nsphere != T::NS || p.ncforce != T::NF || p.nlimit != T::NL || p.nosbody != T::NOS ||
+        p.n_obs_bpos != T::NOBP || p.n_obs_bvel != T::NOBV)
+        return false;
+    if (p.coord_tx != T::TX || p.coord_ty != T::TY || p.coord_tz != T::TZ) return false;
+    if (p.torso_body != T::TORSO || p.calcn_r_body != T::CALCN_R || p.calcn_l_body != T::CALCN_L) return false;
+    if ((p.env_flags & 0x9fu) != T::FLAGS) return false;
+    std::vector<uint32_t> anc(T::NB);
+    for (int c = 0; c < T::NB; ++c) {
+        if (p.cbody[c].parent != T::parent[c]) return false;
+        uint32_t m = 1u << c;
+        for (int q = p.cbody[c].parent; q >= 0; q = p.cbody[q].parent) m |= 1u << q;
+        if (m != T::anc[c]) return false;
+        anc[c] = m;
+        for (int a = 0; a < 6; ++a) {
+            int fi = p.cbody[c].fn[a];
+            int kind = fi < 0 ? -1 : p.fn[fi].type, cc = fi < 0 ? -1 : p.fn[fi].coord;
+            if (kind != T::axis_kind[c * 6 + a] || cc != T::axis_coord[c * 6 + a]) return false;
+        }
+    }
+    for (int c = 0; c < T::NC; ++c)
+        if (p.coord[c].dof != T::coord_dof[c]) return false;
+    for (int c = 0; c < T::NC; ++c) {
+        int d = p.coord[c].dof;
+        if (d >= 0 && (p.coord[c].cbody != T::dof_cb[d] || T::dof_coord[d] != c)) return false;
+    }
+    for (int s = 0; s < T::NS; ++s)
+        if (p.sphere[s].cbody != T::sphere_cb[s] || p.sphere[s].force != T::sphere_force[s]) return false;
+    for (int b = 0; b < T::NOS; ++b)
+        if (p.osbody[b].cbody != T::os_cb[b]) return false;
+    for (int l = 0; l < T::NL; ++l)
+        if (p.limit[l].dof != T::limit_dof[l] || p.limit[l].coord != T::limit_coord[l]) return false;
+    if (p.nmuscle == 0)
+        for (int a = 0; a < T::NA; ++a)
+            if (p.coordact[a].dof != T::act_dof[a] || p.pd_coord[a] != T::pd_coord[a]) return false;
+    for (int b = 0; b < T::NOBP; ++b)
+        if (p.obs_bpos[b] != T::obs_bpos[b]) return false;
+    for (int b = 0; b < T::NOBV; ++b)
+        if (p.obs_bvel[b] != T::obs_bvel[b]) return false;
+    for (int b = 0; b < BIOIM_NREFBODY; ++b)
+        if (p.rw_body[b] != T::rw_body[b]) return false;
+    dofmask.assign(BIOIM_MAX_CBODY, 0);
+    for (int c = 0; c < T::NB; ++c) {
+        dofmask[c] = T::dofmask[c];
+    }
+    return true;
+}
+
+struct Ops {
+    int lanes;
+    size_t lds_bytes_per_env;
+    void (*launch)(bioim_handle_t *, int mode, const void *actions, void *obs, void *reward, uint8_t *done, void *info,
+                   const int32_t *env_ids, const int32_t *ref_index, int n_list);
+};
+
+}  // namespace
+
+struct bioim_handle {
+    int n, device, precision, ndof, nmuscle, nact, horizon, obs_dim, info_dim, nsub, auto_reset;
+    uint64_t seed;
+    hipStream_t stream;
+    bool own_stream;
+    void *model;        /* DModel<Real> on device */
+    void *state_buf;    /* one allocation for every SoA array */
+    size_t state_bytes;
+    void *dstate;       /* DState<Real> (host copy of pointers) */
+    Ops ops;
+    bioim_modelpack_t pack;
+};
+
+namespace {
+
+template <class T, typename Real>
+void launch_impl(bioim_handle_t *h, int mode, const void *actions, void *obs, void *reward, uint8_t *done, void *info,
+                 const int32_t *env_ids, const int32_t *ref_index, int n_list) {
+    constexpr int EPB = 256 / T::G;
+    int count = mode == 1 ? n_list : h->n;
+    int blocks = (count + EPB - 1) / EPB;
+    size_t lds = (size_t)EPB * Lds<T, Real>::SIZE * sizeof(Real);
+    DState<Real> st = *reinterpret_cast<DState<Real> *>(h->dstate);
+    hipLaunchKernelGGL((env_kernel<T, Real>), dim3(blocks), dim3(256), lds, h->stream,
+                       reinterpret_cast<const DModel<Real> *>(h->model), st, h->n, mode,
+                       reinterpret_cast<const Real *>(actions), reinterpret_cast<Real *>(obs),
+                       reinterpret_cast<Real *>(reward), done, reinterpret_cast<Real *>(info), env_ids, ref_index,
+                       n_list, h->auto_reset, h->seed);
+}
+
+template <class T> bool pick(const bioim_modelpack_t &p, int precision, Ops &ops, std::vector<uint32_t> &dofmask) {
+    if (!topology_matches<T>(p, dofmask)) return false;
+    ops.lanes = T::G;
+    if (precision == 64) {
+        ops.launch = &launch_impl<T, double>;
+        ops.lds_bytes_per_env = Lds<T, double>::SIZE * sizeof(double);
+    } else {
+        ops.launch = &launch_impl<T, float>;
+        ops.lds_bytes_per_env = Lds<T, float>::SIZE * sizeof(float);
+    }
+    return true;
+}
+
+template <typename Real> size_t state_layout(bioim_handle_t *h, char *base, DState<Real> *st) {
+    size_t n = h->n, off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off += (bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    size_t oq = take(sizeof(Real) * h->ndof * n), ou = take(sizeof(Real) * h->ndof * n);
+    size_t oa = take(sizeof(Real) * (h->nmuscle ? h->nmuscle : 1) * n), ol = take(sizeof(Real) * (h->nmuscle ? h->nmuscle : 1) * n);
+    size_t oh = take(sizeof(Real) * BIOIM_MAX_HORIZON * h->nact * n), olast = take(sizeof(Real) * h->nact * n);
+    size_t opx = take(sizeof(Real) * n), ot = take(sizeof(double) * n);
+    size_t oi = take(sizeof(int32_t) * n), ohl = take(sizeof(int32_t) * n), od = take(sizeof(int32_t) * n),
+           orr = take(sizeof(int32_t) * n);
+    if (st) {
+        st->q = (Real *)(base + oq); st->u = (Real *)(base + ou); st->act = (Real *)(base + oa);
+        st->lce = (Real *)(base + ol); st->hist = (Real *)(base + oh); st->last = (Real *)(base + olast);
+        st->old_px = (Real *)(base + opx); st->t = (double *)(base + ot); st->istep = (int32_t *)(base + oi);
+        st->has_last = (int32_t *)(base + ohl); st->done = (int32_t *)(base + od); st->resets = (int32_t *)(base + orr);
+    }
+    return off;
+}
+
+template <typename Real> int alloc_state(bioim_handle_t *h) {
+    size_t bytes = state_layout<Real>(h, nullptr, nullptr);
+    HIPCHK(hipMalloc(&h->state_buf, bytes));
+    HIPCHK(hipMemsetAsync(h->state_buf, 0, bytes, h->stream));
+    h->state_bytes = bytes;
+    DState<Real> *st = new DState<Real>();
+    state_layout<Real>(h, (char *)h->state_buf, st);
+    h->dstate = st;
+    DModel<Real> *hm = new DModel<Real>();
+    std::vector<uint32_t> dm(BIOIM_MAX_CBODY, 0);
+    {
+        /* recompute dofmask from the pack (same as the topology's) */
+        for (int c = 0; c < h->pack.ncbody; ++c) {
+            uint32_t anc = 1u << c;
+            for (int q = h->pack.cbody[c].parent; q >= 0; q = h->pack.cbody[q].parent) anc |= 1u << q;
+            uint32_t m = 0;
+            for (int cc = 0; cc < h->pack.ncoord; ++cc) {
+                int d = h->pack.coord[cc].dof;
+                if (d >= 0 && ((anc >> h->pack.coord[cc].cbody) & 1u)) m |= 1u << d;
+            }
+            dm[c] = m;
+        }
+    }
+    convert_model<Real>(h->pack, *hm, dm);
+    HIPCHK(hipMalloc(&h->model, sizeof(DModel<Real>)));
+    HIPCHK(hipMemcpyAsync(h->model, hm, sizeof(DModel<Real>), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    delete hm;
+    return 0;
+}
+
+template <typename Real> int xfer_state(bioim_handle_t *h, double *host, const double *in) {
+    DState<Real> &st = *reinterpret_cast<DState<Real> *>(h->dstate);
+    size_t n = h->n;
+    int nd = h->ndof, nm = h->nmuscle, na = h->nact, H = h->horizon;
+    std::vector<char> buf(h->state_bytes);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipMemcpy(buf.data(), h->state_buf, h->state_bytes, hipMemcpyDeviceToHost));
+    DState<Real> hs;
+    state_layout<Real>(h, buf.data(), &hs);
+    int dim = bioim_state_dim(h);
+    for (size_t e = 0; e < n; ++e) {
+        if (host) {
+            double *s = host + e * dim;
+            int k = 0;
+            s[k++] = hs.t[e]; s[k++] = hs.istep[e]; s[k++] = hs.has_last[e]; s[k++] = hs.old_px[e]; s[k++] = hs.done[e];
+            for (int i = 0; i < nd; ++i) s[k++] = hs.q[i * n + e];
+            for (int i = 0; i < nd; ++i) s[k++] = hs.u[i * n + e];
+            for (int i = 0; i < nm; ++i) s[k++] = hs.act[i * n + e];
+            for (int i = 0; i < nm; ++i) s[k++] = hs.lce[i * n + e];
+            for (int hh = 0; hh < H; ++hh)
+                for (int i = 0; i < na; ++i) s[k++] = hs.hist[(hh * na + i) * n + e];
+            for (int i = 0; i < na; ++i) s[k++] = hs.last[i * n + e];
+        } else {
+            const double *s = in + e * dim;
+            int k = 0;
+            hs.t[e] = s[k++]; hs.istep[e] = (int32_t)s[k++]; hs.has_last[e] = (int32_t)s[k++];
+            hs.old_px[e] = (Real)s[k++]; hs.done[e] = (int32_t)s[k++];
+            for (int i = 0; i < nd; ++i) hs.q[i * n + e] = (Real)s[k++];
+            for (int i = 0; i < nd; ++i) hs.u[i * n + e] = (Real)s[k++];
+            for (int i = 0; i < nm; ++i) hs.act[i * n + e] = (Real)s[k++];
+            for (int i = 0; i < nm; ++i) hs.lce[i * n + e] = (Real)s[k++];
+            for (int hh = 0; hh < H; ++hh)
+                for (int i = 0; i < na; ++i) hs.hist[(hh * na + i) * n + e] = (Real)s[k++];
+            for (int i = 0; i < na; ++i) hs.last[i * n + e] = (Real)s[k++];
+        }
+    }
+    if (in) HIPCHK(hipMemcpy(h->state_buf, buf.data(), h->state_bytes, hipMemcpyHostToDevice));
+    return 0;
+}
+
+}  // namespace
+
+/* ================================================================ C-ABI */
+extern "C" {
+
+const char *bioim_last_error(void) { return g_err.c_str(); }
+uint64_t bioim_modelpack_size(void) { return sizeof(bioim_modelpack_t); }
+
+int bioim_create(const bioim_modelpack_t *pack, int n_envs, int device, int precision, uint64_t seed,
+                 bioim_handle_t **out) {
+    if (!pack || !out || n_envs <= 0) return fail(BIOIM_E_ARG, "bioim_create: bad arguments");
+    if (precision != 32 && precision != 64) return fail(BIOIM_E_ARG, "bioim_create: precision must be 32 or 64");
+    if (pack->magic != BIOIM_PACK_MAGIC || pack->version != BIOIM_PACK_VERSION)
+        return fail(BIOIM_E_PACK, "bioim_create: bad ModelPack magic/version");
+    if (pack->horizon < 1 || pack->horizon > BIOIM_MAX_HORIZON || pack->nsub < 1 || pack->obs_dim > BIOIM_OBS_MAX ||
+        pack->nrows < 2)
+        return fail(BIOIM_E_PACK, "bioim_create: ModelPack env fields out of range");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(BIOIM_E_DEVICE, "bioim_create: no HIP device");
+    if (device < 0 || device >= ndev) return fail(BIOIM_E_DEVICE, "bioim_create: bad device index");
+    HIPCHK(hipSetDevice(device));
+    Ops ops{};
+    std::vector<uint32_t> dofmask;
+    bool found = false;
+#define BIOIM_TRY(S, NAME) \
+    if (!found) found = pick<S>(*pack, precision, ops, dofmask);
+    BIOIM_FOR_EACH_TOPOLOGY(BIOIM_TRY)
+#undef BIOIM_TRY
+    if (!found) return fail(BIOIM_E_NOKERNEL, std::string("bioim_create: no compiled kernel for the topology of ") + pack->env_id);
+    bioim_handle_t *h = new bioim_handle();
+    h->n = n_envs; h->device = device; h->precision = precision; h->seed = seed;
+    h->ndof = pack->ndof; h->nmuscle = pack->nmuscle; h->nact = pack->nact; h->horizon = pack->horizon;
+    h->obs_dim = pack->obs_dim; h->info_dim = pack->info_dim; h->nsub = pack->nsub; h->auto_reset = 0;
+    h->ops = ops;
+    memcpy(&h->pack, pack, sizeof(bioim_modelpack_t));
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return fail(BIOIM_E_DEVICE, "bioim_create: stream creation failed");
+    }
+    h->own_stream = true;
+    int rc = precision == 64 ? alloc_state<double>(h) : alloc_state<float>(h);
+    if (rc) { bioim_destroy(h); return rc; }
+    *out = h;
+    return 0;
+}
+
+int bioim_destroy(bioim_handle_t *h) {
+    if (!h) return 0;
+    if (h->stream) hipStreamSynchronize(h->stream);
+    if (h->state_buf) hipFree(h->state_buf);
+    if (h->model) hipFree(h->model);
+    if (h->dstate) {
+        if (h->precision == 64) delete reinterpret_cast<DState<double> *>(h->dstate);
+        else delete reinterpret_cast<DState<float> *>(h->dstate);
+    }
+    if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
+    delete h;
+    return 0;
+}
+
+int bioim_reset(bioim_handle_t *h, const int32_t *env_ids, const int32_t *ref_index, int n, void *obs) {
+    if (!h) return fail(BIOIM_E_ARG, "bioim_reset: null handle");
+    int count = env_ids ? n : h->n;
+    if (count <= 0) return 0;
+    HIPCHK(hipSetDevice(h->device));
+    h->ops.launch(h, 1, nullptr, obs, nullptr, nullptr, nullptr, env_ids, ref_index, count);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int bioim_step(bioim_handle_t *h, const void *actions, void *obs, void *reward, uint8_t *done, void *info) {
+    if (!h || !actions || !done) return fail(BIOIM_E_ARG, "bioim_step: null handle/actions/done");
+    HIPCHK(hipSetDevice(h->device));
+    h->ops.launch(h, 0, actions, obs, reward, done, info, nullptr, nullptr, 0);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int bioim_set_auto_reset(bioim_handle_t *h, int on) {
+    if (!h) return fail(BIOIM_E_ARG, "null handle");
+    h->auto_reset = on ? 1 : 0;
+    return 0;
+}
+
+int bioim_state_dim(const bioim_handle_t *h) {
+    if (!h) return fail(BIOIM_E_ARG, "null handle");
+    return 5 + 2 * h->ndof + 2 * h->nmuscle + h->horizon * h->nact + h->nact;
+}
+
+int bioim_get_state(bioim_handle_t *h, double *host_state) {
+    if (!h || !host_state) return fail(BIOIM_E_ARG, "bioim_get_state: bad arguments");
+    HIPCHK(hipSetDevice(h->device));
+    return h->precision == 64 ? xfer_state<double>(h, host_state, nullptr) : xfer_state<float>(h, host_state, nullptr);
+}
+
+int bioim_set_state(bioim_handle_t *h, const double *host_state) {
+    if (!h || !host_state) return fail(BIOIM_E_ARG, "bioim_set_state: bad arguments");
+    HIPCHK(hipSetDevice(h->device));
+    return h->precision == 64 ? xfer_state<double>(h, nullptr, host_state) : xfer_state<float>(h, nullptr, host_state);
+}
+
+int bioim_query(const bioim_handle_t *h, int32_t *out) {
+    if (!h || !out) return fail(BIOIM_E_ARG, "bioim_query: bad arguments");
+    out[0] = h->n; out[1] = h->obs_dim; out[2] = h->nact; out[3] = h->info_dim;
+    out[4] = h->precision; out[5] = h->ops.lanes; out[6] = h->nsub; out[7] = bioim_state_dim(h);
+    return 0;
+}
+
+void *bioim_stream(bioim_handle_t *h) { return h ? (void *)h->stream : nullptr; }
+
+int bioim_set_stream(bioim_handle_t *h, void *s) {
+    if (!h) return fail(BIOIM_E_ARG, "null handle");
+    if (h->own_stream && h->stream) {
+        hipStreamSynchronize(h->stream);
+        hipStreamDestroy(h->stream);
+    }
+    h->stream = (hipStream_t)s;
+    h->own_stream = false;
+    return 0;
+}
+
+int bioim_sync(bioim_handle_t *h) {
+    if (!h) return fail(BIOIM_E_ARG, "null handle");
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+}  // extern "C"

@@ -40,6 +40,7 @@ def main():
     a = ap.parse_args()
     ref_data = os.path.join(a.ref, 'bioimitation', 'imitation_envs', 'data')
     os.makedirs(os.path.join(DATA, 'packs'), exist_ok=True)
+    built = []
     for env_id in a.ids:
         recipe = registry.RECIPES[env_id]
         model = load_model(ref_data, recipe)
@@ -54,8 +55,99 @@ def main():
         pk = modelpack.compile_pack(model, spec, ref)
         out = os.path.join(DATA, 'packs', env_id + '.npz')
         np.savez_compressed(out, pack=np.frombuffer(modelpack.pack_bytes(pk), dtype=np.uint8))
+        built.append((env_id, pk))
         print(f'{env_id}: ncoord={pk.ncoord} ndof={pk.ndof} ncbody={pk.ncbody} muscles={pk.nmuscle} '
               f'spheres={pk.nsphere} limits={pk.nlimit} act={pk.nact} obs={pk.obs_dim} rows={pk.nrows} -> {out}')
+    write_topologies(built)
+
+
+
+
+# --------------------------------------------------------------------------
+# compile-time topology descriptors for the HIP kernels (csrc/topologies.h)
+def _carr(name, vals, ctype='int'):
+    vals = list(vals) or [0]
+    return f'    static constexpr {ctype} {name}[{len(vals)}] = {{{", ".join(str(int(v)) for v in vals)}}};\n'
+
+
+def emit_topology(struct, pk, lanes):
+    nb, nd, nc, nm = pk.ncbody, pk.ndof, pk.ncoord, pk.nmuscle
+    parent = [pk.cbody[c].parent for c in range(nb)]
+    anc = []
+    for c in range(nb):
+        m, p = 1 << c, parent[c]
+        while p >= 0:
+            m |= 1 << p
+            p = parent[p]
+        anc.append(m)
+    dof_cb = [0] * max(nd, 1)
+    dof_coord = [0] * max(nd, 1)
+    for c in range(nc):
+        d = pk.coord[c].dof
+        if d >= 0:
+            dof_cb[d] = pk.coord[c].cbody
+            dof_coord[d] = c
+    dofmask = []
+    for c in range(nb):
+        m = 0
+        for d in range(nd):
+            if anc[c] >> dof_cb[d] & 1:
+                m |= 1 << d
+        dofmask.append(m)
+    axis_coord, axis_kind = [], []
+    for c in range(nb):
+        for a in range(6):
+            fi = pk.cbody[c].fn[a]
+            axis_kind.append(-1 if fi < 0 else pk.fn[fi].type)
+            axis_coord.append(-1 if fi < 0 else pk.fn[fi].coord)
+    s = f'struct {struct} {{\n'
+    s += f'    static constexpr int NB = {nb}, ND = {nd}, NC = {nc}, NM = {nm}, NA = {pk.nact}, NS = {pk.nsphere},' \
+         f' NF = {pk.ncforce}, NL = {pk.nlimit}, NOS = {pk.nosbody}, G = {lanes};\n'
+    s += f'    static constexpr int NOBP = {pk.n_obs_bpos}, NOBV = {pk.n_obs_bvel};\n'
+    s += f'    static constexpr int TX = {pk.coord_tx}, TY = {pk.coord_ty}, TZ = {pk.coord_tz};\n'
+    s += f'    static constexpr int TORSO = {pk.torso_body}, CALCN_R = {pk.calcn_r_body}, CALCN_L = {pk.calcn_l_body};\n'
+    s += f'    static constexpr unsigned FLAGS = {pk.env_flags & 0x9f}u; /* structural env flags */\n'
+    s += _carr('parent', parent) + _carr('anc', anc, 'unsigned') + _carr('dofmask', dofmask, 'unsigned')
+    s += _carr('coord_dof', [pk.coord[c].dof for c in range(nc)])
+    s += _carr('dof_cb', dof_cb) + _carr('dof_coord', dof_coord)
+    s += _carr('axis_kind', axis_kind) + _carr('axis_coord', axis_coord)
+    s += _carr('sphere_cb', [pk.sphere[i].cbody for i in range(pk.nsphere)])
+    s += _carr('sphere_force', [pk.sphere[i].force for i in range(pk.nsphere)])
+    s += _carr('os_cb', [pk.osbody[i].cbody for i in range(pk.nosbody)])
+    s += _carr('limit_dof', [pk.limit[i].dof for i in range(pk.nlimit)])
+    s += _carr('limit_coord', [pk.limit[i].coord for i in range(pk.nlimit)])
+    s += _carr('act_dof', [pk.coordact[i].dof for i in range(pk.ncoordact)] if pk.ncoordact else [-1])
+    s += _carr('pd_coord', [pk.pd_coord[i] for i in range(pk.nact)])
+    s += _carr('obs_bpos', [pk.obs_bpos[i] for i in range(pk.n_obs_bpos)])
+    s += _carr('obs_bvel', [pk.obs_bvel[i] for i in range(pk.n_obs_bvel)])
+    s += _carr('rw_body', [pk.rw_body[i] for i in range(9)])
+    s += '};\n'
+    return s
+
+
+def topology_signature(pk):
+    """Everything the compiled kernels bake in; bioim_create() recomputes it
+    from the pack and refuses a pack whose signature has no kernel."""
+    import hashlib
+    return hashlib.sha1(emit_topology('T', pk, 0).encode()).hexdigest()[:16]
+
+
+def write_topologies(packs):
+    out = ['/* GENERATED by tools/build_packs.py — compile-time topology of each env family. */',
+           '#pragma once', '']
+    names = []
+    for env_id, pk in packs:
+        struct = 'Topo_' + env_id.replace('-', '_')
+        lanes = 16 if max(pk.nmuscle, pk.nact, pk.ncoord) <= 16 else 32
+        out.append(emit_topology(struct, pk, lanes))
+        names.append((env_id, struct))
+    out.append('#define BIOIM_FOR_EACH_TOPOLOGY(X) \\')
+    out.append(' \\\n'.join(f'    X({s}, "{e}")' for e, s in names))
+    out.append('')
+    path = os.path.join(PKG_ROOT, 'csrc', 'topologies.h')
+    with open(path, 'w') as fh:
+        fh.write('\n'.join(out))
+    print('wrote', path)
 
 
 if __name__ == '__main__':

@@ -1,0 +1,102 @@
+/*
+ * bioim.h — C-ABI of the MI355X-native vectorized env step (libbioim.so).
+ *
+ * This is the drop-in boundary for the reference's physics facade
+ * `OsimModel` (bioimitation/imitation_envs/utils/opensim_wrapper.py:6-338)
+ * plus the per-step env arithmetic layered on it by the task envs
+ * (muscle_walking_imitation_env2D.py:115-403, torque_walking_imitation_env2D.py:117-366)
+ * and by `OsimEnv.step/reset` (opensim_environment.py:86-113).  One handle
+ * owns N independent environment instances of one registered env ID on one
+ * GPU; every call advances/reads all of them (a batched `env.step`).
+ *
+ * Each entry point cites the reference interface it replaces:
+ *
+ *   bioim_create   <- OsimEnv.__init__ -> OsimModel.__init__ (opensim_wrapper.py:7-90),
+ *                     per instance, N times
+ *   bioim_reset    <- Env.reset (muscle_walking_imitation_env2D.py:133-156) =
+ *                     OsimModel.reset/set_time/set_coordinates/set_velocities
+ *                     (opensim_wrapper.py:293-332) + get_observation
+ *   bioim_step     <- Env.step (muscle_walking_imitation_env2D.py:115-131) ->
+ *                     OsimEnv.step (opensim_environment.py:100-113) =
+ *                     actuate (opensim_wrapper.py:92-107) + integrate (:299-301)
+ *                     + get_state_dict/get_reward/is_done
+ *   bioim_get_state/bioim_set_state <- (no reference equivalent; the env
+ *                     state is not checkpointable upstream) parity re-sync,
+ *                     checkpoint/resume
+ *   bioim_destroy  <- garbage collection of the OsimModel instances
+ *
+ * Conventions
+ *   - Real-valued buffers are float (precision 32) or double (precision 64),
+ *     fixed at create time.  All buffers passed to reset/step are DEVICE
+ *     pointers on the handle's device; the caller owns them.
+ *   - obs is [N][obs_dim] row-major, reward [N], done [N] (uint8 0/1),
+ *     info [N][info_dim] (the reference's info['all_rewards']).
+ *   - Calls are asynchronous on the handle's HIP stream (bioim_stream /
+ *     bioim_set_stream); bioim_sync waits.  Not re-entrant per handle.
+ *   - Every entry returns 0 on success, < 0 on error; bioim_last_error()
+ *     returns the thread-local message.  A missing GPU or a pack whose
+ *     topology has no compiled kernel is an error (there is no CPU fallback).
+ *
+ * Flat per-env state (bioim_get_state/set_state, doubles), matching the
+ * oracle's layout: [t, istep, has_last, old_pelvis_x, done, q[ndof], u[ndof],
+ * activation[nmuscle], fiber_length[nmuscle], hist[horizon][nact],
+ * last_action[nact]].
+ */
+#ifndef BIOIM_H
+#define BIOIM_H
+
+#include <stdint.h>
+
+#include "bioim_modelpack.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct bioim_handle bioim_handle_t;
+
+enum {
+    BIOIM_OK = 0,
+    BIOIM_E_ARG = -1,
+    BIOIM_E_DEVICE = -2,
+    BIOIM_E_PACK = -3,
+    BIOIM_E_NOKERNEL = -4,
+    BIOIM_E_LAUNCH = -5,
+};
+
+/* Create N env instances of the pack's env ID on `device`; precision 32|64.
+ * `seed` drives reset indices drawn on the device (randint(0, reset_hi)). */
+int bioim_create(const bioim_modelpack_t *pack, int n_envs, int device, int precision, uint64_t seed,
+                 bioim_handle_t **out);
+int bioim_destroy(bioim_handle_t *h);
+
+/* Reset `n` envs.  env_ids: device int32[n] (NULL = all envs, n ignored).
+ * ref_index: device int32[n] reference-row indices (NULL = draw
+ * randint(0, reset_hi) per env from the handle's counter-based RNG).
+ * obs (may be NULL): device [N][obs_dim] — rows of the reset envs are written. */
+int bioim_reset(bioim_handle_t *h, const int32_t *env_ids, const int32_t *ref_index, int n, void *obs);
+
+/* One env step for all N envs.  actions: device [N][nact].  Outputs may be
+ * NULL except done.  With auto-reset on, envs that finish are reset in the
+ * same launch and their obs row is the post-reset observation. */
+int bioim_step(bioim_handle_t *h, const void *actions, void *obs, void *reward, uint8_t *done, void *info);
+int bioim_set_auto_reset(bioim_handle_t *h, int on);
+
+/* Host-side state transfer (synchronous). */
+int bioim_state_dim(const bioim_handle_t *h);
+int bioim_get_state(bioim_handle_t *h, double *host_state /* [N][state_dim] */);
+int bioim_set_state(bioim_handle_t *h, const double *host_state);
+
+/* out[0..7] = n_envs, obs_dim, nact, info_dim, precision, lanes_per_env, nsub, state_dim */
+int bioim_query(const bioim_handle_t *h, int32_t *out);
+void *bioim_stream(bioim_handle_t *h);
+int bioim_set_stream(bioim_handle_t *h, void *hip_stream);
+int bioim_sync(bioim_handle_t *h);
+const char *bioim_last_error(void);
+/* sizeof(bioim_modelpack_t) as compiled into the library (layout check). */
+uint64_t bioim_modelpack_size(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BIOIM_H */
