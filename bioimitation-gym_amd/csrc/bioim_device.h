@@ -11,10 +11,14 @@
 
 #define BIOIM_OBS_MAX 256
 
+#define BIOIM_UTAB 32 /* intervals of the per-segment u(x) initial-guess table */
+
 template <typename Real>
 struct DCurve {
     Real x[BIOIM_MAX_CURVESEG][6];
     Real y[BIOIM_MAX_CURVESEG][6];
+    Real ut[BIOIM_MAX_CURVESEG][BIOIM_UTAB + 1]; /* u at uniform x nodes of each segment */
+    Real inv_h[BIOIM_MAX_CURVESEG];               /* BIOIM_UTAB / (x_end - x_start)       */
     Real x0, y0, dydx0, x1, y1, dydx1;
     int32_t nseg, pad;
 };
@@ -64,6 +68,15 @@ struct DModel {
         lim_damp[BIOIM_MAX_LIMIT], lim_trans[BIOIM_MAX_LIMIT];
     Real ca_opt[BIOIM_MAX_ACT], ca_min[BIOIM_MAX_ACT], ca_max[BIOIM_MAX_ACT];
     Real kp[BIOIM_MAX_ACT], kv[BIOIM_MAX_ACT];
+    /* lane-parallel index tables (runtime copies of the topology) */
+    uint32_t anc[BIOIM_MAX_CBODY], dofmask[BIOIM_MAX_CBODY];
+    int32_t dof_cb[BIOIM_MAX_COORD];
+    int32_t e_l[BIOIM_MAX_COORD * (BIOIM_MAX_COORD + 1) / 2], e_k[BIOIM_MAX_COORD * (BIOIM_MAX_COORD + 1) / 2],
+        e_c[BIOIM_MAX_COORD * (BIOIM_MAX_COORD + 1) / 2];
+    int32_t sph_cb[BIOIM_MAX_SPHERE], sph_force[BIOIM_MAX_SPHERE];
+    int32_t lim_coord[BIOIM_MAX_LIMIT], lim_dof[BIOIM_MAX_LIMIT];
+    int32_t act_dof[BIOIM_MAX_ACT];
+    int32_t float_origin, pad1;
     /* env semantics */
     Real w_imitate, w_effort, w_action, action_r_scale, max_actuation, total_mass, weight, moment;
     Real torso_y_min, limit_force_max, acc_max;

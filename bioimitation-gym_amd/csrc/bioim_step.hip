@@ -157,52 +157,59 @@ template <typename Real> DEV Real dbez5(const Real *p, Real u) {
                       Real(6) * (p[3] - p[2]) * u2 * v2 + Real(4) * (p[4] - p[3]) * u2 * u * v + (p[5] - p[4]) * u2 * u2);
 }
 
-/* y(x), dy/dx: segment located branch-free, x(u) inverted by bracketed Newton */
+/* y(x), dy/dx of a SmoothSegmentedFunction.  Branch-free with a fixed trip
+ * count (no lane divergence): segment located by comparisons, u(x) started
+ * from the segment's 32-interval table by linear interpolation, then exactly
+ * three Newton steps on the quintic x(u) (converges to machine precision,
+ * see tests/test_curves.py); linear extrapolation outside [x0, x1]. */
 template <typename Real>
 DEV void curve_eval(const DCurve<Real> &C, Real x, Real &y, Real &dydx) {
-    if (x <= C.x0) { y = C.y0 + C.dydx0 * (x - C.x0); dydx = C.dydx0; return; }
-    if (x >= C.x1) { y = C.y1 + C.dydx1 * (x - C.x1); dydx = C.dydx1; return; }
+    Real xc = x < C.x0 ? C.x0 : (x > C.x1 ? C.x1 : x);
     int k = 0;
-    for (int s = 0; s < C.nseg - 1; ++s) k += (x > C.x[s][5]) ? 1 : 0;
+    for (int s = 0; s < C.nseg - 1; ++s) k += (xc > C.x[s][5]) ? 1 : 0;
     Real px[6], py[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) { px[i] = C.x[k][i]; py[i] = C.y[k][i]; }
-    Real lo = 0, hi = 1, u = (x - px[0]) / (px[5] - px[0]);
-    for (int it = 0; it < Eps<Real>::it_max; ++it) {
-        Real f = bez5(px, u) - x;
-        if (f > 0) hi = u; else lo = u;
-        Real d = dbez5(px, u);
-        Real un = u - f / d;
-        if (!(un > lo && un < hi)) un = Real(0.5) * (lo + hi);
-        Real du = un - u;
-        u = un;
-        if (fabs(du) <= Eps<Real>::u_tol) break;
-    }
+    Real tt = (xc - px[0]) * C.inv_h[k];
+    int i0 = (int)tt;
+    i0 = i0 < 0 ? 0 : (i0 > BIOIM_UTAB - 1 ? BIOIM_UTAB - 1 : i0);
+    Real fr = tt - Real(i0);
+    Real u = C.ut[k][i0] + fr * (C.ut[k][i0 + 1] - C.ut[k][i0]);
+#pragma unroll
+    for (int it = 0; it < 3; ++it) u -= (bez5(px, u) - xc) / dbez5(px, u);
     y = bez5(py, u);
     dydx = dbez5(py, u) / dbez5(px, u);
+    if (x < C.x0) { y = C.y0 + C.dydx0 * (x - C.x0); dydx = C.dydx0; }
+    if (x > C.x1) { y = C.y1 + C.dydx1 * (x - C.x1); dydx = C.dydx1; }
 }
 
-/* root of a*fal*fv(v) + beta*v = rhs (increasing in v), solved directly in
- * the Bezier parameter of the bracketing segment; returns v, fv, dfv/dv */
+/* root of a*fal*fv(v) + beta*v = rhs (strictly increasing in v), solved in the
+ * Bezier parameter of the bracketing segment, warm-started from v0 (the
+ * previous substep's root) through the segment's u(x) table; returns v, fv,
+ * dfv/dv.  Four safeguarded Newton steps, then (rarely) more until
+ * converged. */
 template <typename Real>
-DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real &v, Real &fv, Real &dfv) {
+DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0, Real &v, Real &fv, Real &dfv) {
     Real g0 = afal * C.y0 + beta * C.x0 - rhs;
-    if (g0 >= 0) {
-        v = (rhs - afal * (C.y0 - C.dydx0 * C.x0)) / (afal * C.dydx0 + beta);
-        fv = C.y0 + C.dydx0 * (v - C.x0); dfv = C.dydx0; return;
-    }
     Real g1 = afal * C.y1 + beta * C.x1 - rhs;
-    if (g1 <= 0) {
-        v = (rhs - afal * (C.y1 - C.dydx1 * C.x1)) / (afal * C.dydx1 + beta);
-        fv = C.y1 + C.dydx1 * (v - C.x1); dfv = C.dydx1; return;
-    }
     int k = 0;
     for (int s = 1; s < C.nseg; ++s) k += (afal * C.y[s][0] + beta * C.x[s][0] - rhs <= 0) ? 1 : 0;
     Real px[6], py[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) { px[i] = C.x[k][i]; py[i] = C.y[k][i]; }
     Real ga = afal * py[0] + beta * px[0] - rhs, gb = afal * py[5] + beta * px[5] - rhs;
-    Real lo = 0, hi = 1, u = ga / (ga - gb);
+    Real u;
+    if (v0 > px[0] && v0 < px[5]) {
+        Real tt = (v0 - px[0]) * C.inv_h[k];
+        int i0 = (int)tt;
+        i0 = i0 < 0 ? 0 : (i0 > BIOIM_UTAB - 1 ? BIOIM_UTAB - 1 : i0);
+        Real fr = tt - Real(i0);
+        u = C.ut[k][i0] + fr * (C.ut[k][i0 + 1] - C.ut[k][i0]);
+    } else {
+        u = ga / (ga - gb);
+    }
+    u = u > Real(0) && u < Real(1) ? u : Real(0.5);
+    Real lo = 0, hi = 1;
     for (int it = 0; it < Eps<Real>::it_max; ++it) {
         Real g = afal * bez5(py, u) + beta * bez5(px, u) - rhs;
         if (g > 0) hi = u; else lo = u;
@@ -211,53 +218,114 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real &v
         if (!(un > lo && un < hi)) un = Real(0.5) * (lo + hi);
         Real du = un - u;
         u = un;
-        if (fabs(du) <= Eps<Real>::u_tol) break;
+        if (it >= 3 && fabs(du) <= Eps<Real>::u_tol) break;
     }
     v = bez5(px, u);
     fv = bez5(py, u);
     dfv = dbez5(py, u) / dbez5(px, u);
+    if (g0 >= 0) {
+        v = (rhs - afal * (C.y0 - C.dydx0 * C.x0)) / (afal * C.dydx0 + beta);
+        fv = C.y0 + C.dydx0 * (v - C.x0); dfv = C.dydx0;
+    } else if (g1 <= 0) {
+        v = (rhs - afal * (C.y1 - C.dydx1 * C.x1)) / (afal * C.dydx1 + beta);
+        fv = C.y1 + C.dydx1 * (v - C.x1); dfv = C.dydx1;
+    }
 }
 
-/* ---------------------------------------------------------- kinematics */
+/* ---------------------------------------------------------- LDS layout
+ * One region per env (4 envs per 64-lane workgroup).  Phase 1 (streamed
+ * kinematics, redundant in every lane) publishes the composite frames, the
+ * Plucker columns, per-body inertias and Newton-Euler wrenches; the
+ * lane-parallel phases read them and publish per-lane force slots that are
+ * reduced in a fixed order (bitwise deterministic). */
+template <class T, typename Real> struct Lay {
+    static constexpr int NB = T::NB, ND = T::ND > 0 ? T::ND : 1, NC = T::NC, NP = ND * (ND + 1) / 2;
+    static constexpr int NMS = T::NM > T::NA ? T::NM : T::NA;
+    static constexpr int NS = T::NS > 0 ? T::NS : 1, NL = T::NL > 0 ? T::NL : 1;
+    static constexpr int KB = 0;                 /* [NB][18]: R9 o3 w3 vO3      */
+    static constexpr int S = KB + 18 * NB;       /* [ND][6]: Omega, Vo          */
+    static constexpr int QF = S + 6 * ND;        /* [NC] coordinate values       */
+    static constexpr int IC = QF + NC;           /* [NB][10]: m, h3, J6          */
+    static constexpr int WB = IC + 10 * NB;      /* [NB][6]: n3, f3              */
+    static constexpr int ICS = WB + 6 * NB;      /* subtree sums of IC           */
+    static constexpr int WBS = ICS + 10 * NB;    /* subtree sums of WB           */
+    static constexpr int MP = WBS + 6 * NB;      /* [NP] packed lower M (+implicit) */
+    static constexpr int RHS = MP + NP;          /* [ND]                         */
+    static constexpr int TAU = RHS + ND;         /* [NMS][ND] muscle/actuator slots */
+    static constexpr int CT = TAU + NMS * ND;    /* [NS][ND] contact tau slots   */
+    static constexpr int CM = CT + NS * ND;      /* [NS][NP] contact implicit slots */
+    static constexpr int CW = CM + NS * NP;      /* [NS][8]: F3, Mo3, active     */
+    static constexpr int LIM = CW + 8 * NS;      /* [NL][4]: f, diag add, tau add */
+    static constexpr int OBS = ((LIM + 4 * NL + 1) / 2) * 2;
+    static constexpr int SIZE = ((OBS + BIOIM_OBS_MAX + 1) / 2) * 2;
+};
+
+DEV void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+/* Diagnostic build only (-DBIOIM_STAMPS, tools/stamps.py): per-phase shader
+ * cycles of the first env of workgroup 0, accumulated over one launch. */
+#ifdef BIOIM_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define STAMP(i)                                                                      \
+    do {                                                                              \
+        __builtin_amdgcn_sched_barrier(0);                                            \
+        unsigned long long t_ = __builtin_amdgcn_s_memtime();                         \
+        __builtin_amdgcn_s_waitcnt(0xC07F);                                           \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[i] += t_ - stamp_prev;      \
+        stamp_prev = t_;                                                              \
+        __builtin_amdgcn_sched_barrier(0);                                            \
+    } while (0)
+#define STAMP_DECL unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
+#else
+#define STAMP(i) do {} while (0)
+#define STAMP_DECL
+#endif
+
 template <typename Real> struct Kin {
     Real R[9], o[3], w[3], vO[3], al[3], aO[3];
 };
 
-template <class T, typename Real> struct Work {
-    static constexpr int ND = T::ND > 0 ? T::ND : 1;
-    static constexpr int NP = ND * (ND + 1) / 2;
-    Kin<Real> K[T::NB];
-    Real S[ND][6];
-    Real qf[T::NC], uf[T::NC];
-};
-
 template <int I> DEV constexpr int tri(int k, int l) { return k * (k + 1) / 2 + l; }
 
+/* coordinate values/speeds (locked: default / 0) */
 template <class T, typename Real>
-DEV void fill_coords(const DModel<Real> &M, const Real *q, const Real *u, Work<T, Real> &W) {
+DEV void fill_coords(const DModel<Real> &M, const Real *q, const Real *u, Real *qf, Real *uf) {
     sfor<0, T::NC>([&](auto cI) {
         constexpr int c = decltype(cI)::value;
         constexpr int d = T::coord_dof[c];
-        if constexpr (d >= 0) { W.qf[c] = q[d]; W.uf[c] = u[d]; }
-        else { W.qf[c] = M.coord_default[c]; W.uf[c] = 0; }
+        if constexpr (d >= 0) { qf[c] = q[d]; uf[c] = u[d]; }
+        else { qf[c] = M.coord_default[c]; uf[c] = 0; }
     });
 }
 
+/* Phase 1: streamed kinematics.  Every lane computes the whole tree in
+ * registers (compile-time topology; a body's registers die after its last
+ * child); lane 0 publishes per body: frame + spatial velocity, the Plucker
+ * columns of its dofs, its spatial inertia at the ground origin and its
+ * Newton-Euler (velocity-product + gravity) wrench.  The ground-x origin is
+ * shifted by x0 (floating origin; dynamics are invariant to it). */
 template <class T, typename Real>
-DEV void kinematics(const DModel<Real> &M, Work<T, Real> &W) {
+DEV void kinematics(const DModel<Real> &M, const Real *qf, const Real *uf, Real x0, Real (&S)[Lay<T, Real>::ND][6],
+                    Real *lds, bool publish) {
+    using LY = Lay<T, Real>;
+    Kin<Real> K[T::NB];
     sfor<0, T::NB>([&](auto cI) {
         constexpr int c = decltype(cI)::value;
         constexpr int p = T::parent[c];
-        Kin<Real> &k = W.K[c];
-        Real RP[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, oP[3] = {0, 0, 0}, wP[3] = {0, 0, 0}, vOP[3] = {0, 0, 0},
+        Kin<Real> &k = K[c];
+        Real RP[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, oP[3] = {-x0, 0, 0}, wP[3] = {0, 0, 0}, vOP[3] = {0, 0, 0},
              alP[3] = {0, 0, 0}, aOP[3] = {0, 0, 0};
         if constexpr (p >= 0) {
 #pragma unroll
-            for (int i = 0; i < 9; ++i) RP[i] = W.K[p].R[i];
+            for (int i = 0; i < 9; ++i) RP[i] = K[p].R[i];
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                oP[i] = W.K[p].o[i]; wP[i] = W.K[p].w[i]; vOP[i] = W.K[p].vO[i];
-                alP[i] = W.K[p].al[i]; aOP[i] = W.K[p].aO[i];
+                oP[i] = K[p].o[i]; wP[i] = K[p].w[i]; vOP[i] = K[p].vO[i];
+                alP[i] = K[p].al[i]; aOP[i] = K[p].aO[i];
             }
         }
         Real RGF[9], oF[3], vF[3], aF[3], t[3], t2[3];
@@ -283,7 +351,7 @@ DEV void kinematics(const DModel<Real> &M, Work<T, Real> &W) {
             mv3(RFM, M.axis[c][ax], ucol[ax]);
             if constexpr (kind >= 0) {
                 Real qc = 0, uc = 0;
-                if constexpr (cc >= 0) { qc = W.qf[cc]; uc = W.uf[cc]; }
+                if constexpr (cc >= 0) { qc = qf[cc]; uc = uf[cc]; }
                 Real f, f1, f2;
                 fn_eval_ct<kind>(M, M.fn[c][ax], qc, f, f1, f2);
                 f1s[ax] = f1;
@@ -304,7 +372,7 @@ DEV void kinematics(const DModel<Real> &M, Work<T, Real> &W) {
             constexpr int cc = T::axis_coord[c * 6 + ax];
             if constexpr (kind >= 0) {
                 Real qc = 0, uc = 0;
-                if constexpr (cc >= 0) { qc = W.qf[cc]; uc = W.uf[cc]; }
+                if constexpr (cc >= 0) { qc = qf[cc]; uc = uf[cc]; }
                 Real f, f1, f2;
                 fn_eval_ct<kind>(M, M.fn[c][ax], qc, f, f1, f2);
                 f1s[ax] = f1;
@@ -364,7 +432,6 @@ DEV void kinematics(const DModel<Real> &M, Work<T, Real> &W) {
 #pragma unroll
             for (int i = 0; i < 3; ++i) k.aO[i] = aB[i] - a1[i] - a2[i];
         }
-        /* Plucker columns of the dofs of this joint */
         sfor<0, T::ND>([&](auto dI) {
             constexpr int d = decltype(dI)::value;
             if constexpr (T::dof_cb[d] == c) {
@@ -389,134 +456,74 @@ DEV void kinematics(const DModel<Real> &M, Work<T, Real> &W) {
                 mv3(RGF, Vm, VG);
                 cross3(OG, oM, tt);
 #pragma unroll
-                for (int i = 0; i < 3; ++i) { W.S[d][i] = OG[i]; W.S[d][3 + i] = VG[i] - tt[i]; }
+                for (int i = 0; i < 3; ++i) { S[d][i] = OG[i]; S[d][3 + i] = VG[i] - tt[i]; }
+                if (publish) {
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) lds[LY::S + 6 * d + i] = S[d][i];
+                }
             }
         });
-    });
-}
-
-/* velocity of the material point of composite c at ground point P */
-template <typename Real> DEV void point_vel(const Kin<Real> &k, const Real *P, Real *v) {
-    Real t[3];
-    cross3(k.w, P, t);
+        if (publish) {
+            Real *kb = lds + LY::KB + 18 * c;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) v[i] = k.vO[i] + t[i];
-}
-
-/* tau += J_P^T F for a point force on composite c (dofs in dofmask[c]) */
-template <class T, int C, typename Real>
-DEV void point_force(const Work<T, Real> &W, const Real *P, const Real *F, Real *tau) {
-    Real m[3];
-    cross3(P, F, m);
-    sfor<0, T::ND>([&](auto dI) {
-        constexpr int d = decltype(dI)::value;
-        if constexpr ((T::dofmask[C] >> d) & 1u) tau[d] += dot3(W.S[d], m) + dot3(W.S[d] + 3, F);
-    });
-}
-
-/* ------------------------------------------------ mass matrix and bias */
-template <class T, typename Real>
-DEV void mass_bias(const DModel<Real> &M, const Work<T, Real> &W, Real *Mp, Real *bias) {
-    constexpr int NB = T::NB;
-    Real Jc[NB][9], hc[NB][3], mc[NB], Wn[NB][3], Wf[NB][3];
-    sfor<0, NB>([&](auto cI) {
-        constexpr int c = decltype(cI)::value;
-        const Kin<Real> &k = W.K[c];
-        Real cl[3], cG[3];
-        mv3(k.R, M.com[c], cl);
+            for (int i = 0; i < 9; ++i) kb[i] = k.R[i];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) cG[i] = k.o[i] + cl[i];
-        /* IG = R Ib R^T */
-        Real Ib[9] = {M.inertia[c][0], M.inertia[c][3], M.inertia[c][4], M.inertia[c][3], M.inertia[c][1],
-                      M.inertia[c][5], M.inertia[c][4], M.inertia[c][5], M.inertia[c][2]};
-        Real Tm[9], RT[9], IG[9];
+            for (int i = 0; i < 3; ++i) { kb[9 + i] = k.o[i]; kb[12 + i] = k.w[i]; kb[15 + i] = k.vO[i]; }
+            /* spatial inertia at the ground origin and the Newton-Euler wrench */
+            Real cl[3], cG[3];
+            mv3(k.R, M.com[c], cl);
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
+            for (int i = 0; i < 3; ++i) cG[i] = k.o[i] + cl[i];
+            Real Ib[9] = {M.inertia[c][0], M.inertia[c][3], M.inertia[c][4], M.inertia[c][3], M.inertia[c][1],
+                          M.inertia[c][5], M.inertia[c][4], M.inertia[c][5], M.inertia[c][2]};
+            Real Tm[9], RT[9], IG[9];
 #pragma unroll
-            for (int j = 0; j < 3; ++j) RT[3 * i + j] = k.R[3 * j + i];
-        mm3(k.R, Ib, Tm);
-        mm3(Tm, RT, IG);
-        Real m = M.mass[c];
-        mc[c] = m;
+            for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int i = 0; i < 3; ++i) hc[c][i] = m * cG[i];
-        Real cc = dot3(cG, cG);
+                for (int j = 0; j < 3; ++j) RT[3 * i + j] = k.R[3 * j + i];
+            mm3(k.R, Ib, Tm);
+            mm3(Tm, RT, IG);
+            Real m = M.mass[c], ccd = dot3(cG, cG);
+            Real *ic = lds + LY::IC + 10 * c;
+            ic[0] = m;
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
+            for (int i = 0; i < 3; ++i) ic[1 + i] = m * cG[i];
+            ic[4] = IG[0] + m * (ccd - cG[0] * cG[0]);
+            ic[5] = IG[4] + m * (ccd - cG[1] * cG[1]);
+            ic[6] = IG[8] + m * (ccd - cG[2] * cG[2]);
+            ic[7] = IG[1] - m * cG[0] * cG[1];
+            ic[8] = IG[2] - m * cG[0] * cG[2];
+            ic[9] = IG[5] - m * cG[1] * cG[2];
+            Real vc[3], ac[3];
+            cross3(k.w, cG, t);
 #pragma unroll
-            for (int j = 0; j < 3; ++j) Jc[c][3 * i + j] = IG[3 * i + j] + m * ((i == j ? cc : Real(0)) - cG[i] * cG[j]);
-        Real vc[3], ac[3], t[3], t2[3];
-        cross3(k.w, cG, t);
+            for (int i = 0; i < 3; ++i) vc[i] = k.vO[i] + t[i];
+            cross3(k.al, cG, t);
+            cross3(k.w, vc, t2);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) vc[i] = k.vO[i] + t[i];
-        cross3(k.al, cG, t);
-        cross3(k.w, vc, t2);
+            for (int i = 0; i < 3; ++i) ac[i] = k.aO[i] + t[i] + t2[i];
+            Real f[3], Iw[3], Ia[3], n[3];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) ac[i] = k.aO[i] + t[i] + t2[i];
-        Real f[3], Iw[3], Ia[3], n[3];
+            for (int i = 0; i < 3; ++i) f[i] = m * (ac[i] - M.gravity[i]);
+            mv3(IG, k.w, Iw);
+            mv3(IG, k.al, Ia);
+            cross3(k.w, Iw, t);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) f[i] = m * (ac[i] - M.gravity[i]);
-        mv3(IG, k.w, Iw);
-        mv3(IG, k.al, Ia);
-        cross3(k.w, Iw, t);
+            for (int i = 0; i < 3; ++i) n[i] = Ia[i] + t[i];
+            cross3(cG, f, t);
+            Real *wb = lds + LY::WB + 6 * c;
 #pragma unroll
-        for (int i = 0; i < 3; ++i) n[i] = Ia[i] + t[i];
-        cross3(cG, f, t);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) { Wn[c][i] = n[i] + t[i]; Wf[c][i] = f[i]; }
-    });
-    sfor<0, NB>([&](auto iI) {
-        constexpr int c = NB - 1 - decltype(iI)::value;
-        constexpr int p = T::parent[c];
-        if constexpr (p >= 0) {
-            mc[p] += mc[c];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) { hc[p][i] += hc[c][i]; Wn[p][i] += Wn[c][i]; Wf[p][i] += Wf[c][i]; }
-#pragma unroll
-            for (int i = 0; i < 9; ++i) Jc[p][i] += Jc[c][i];
+            for (int i = 0; i < 3; ++i) { wb[i] = n[i] + t[i]; wb[3 + i] = f[i]; }
         }
     });
-    sfor<0, T::ND>([&](auto dI) {
-        constexpr int d = decltype(dI)::value;
-        constexpr int c = T::dof_cb[d];
-        bias[d] = dot3(W.S[d], Wn[c]) + dot3(W.S[d] + 3, Wf[c]);
-    });
-    sfor<0, T::ND>([&](auto lI) {
-        constexpr int l = decltype(lI)::value;
-        constexpr int cl = T::dof_cb[l];
-        const Real *Sl = W.S[l];
-        /* momentum of the composite below l's body per unit u_l */
-        Real L[3], Pm[3], t[3];
-        mv3(Jc[cl], Sl, L);
-        cross3(hc[cl], Sl + 3, t);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) L[i] += t[i];
-        cross3(Sl, hc[cl], t);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) Pm[i] = mc[cl] * Sl[3 + i] + t[i];
-        sfor<0, l + 1>([&](auto kI) {
-            constexpr int k = decltype(kI)::value;
-            constexpr int ck = T::dof_cb[k];
-            if constexpr ((T::anc[cl] >> ck) & 1u) {
-                Mp[tri<0>(l, k)] = dot3(W.S[k], L) + dot3(W.S[k] + 3, Pm);
-            } else if constexpr ((T::anc[ck] >> cl) & 1u) {
-                /* cl is an ancestor of ck (k < l cannot be deeper in a topological
-                 * dof order unless on another branch) — computed from ck's side */
-                Real L2[3], P2[3], t3[3];
-                const Real *Sk = W.S[k];
-                mv3(Jc[ck], Sk, L2);
-                cross3(hc[ck], Sk + 3, t3);
-#pragma unroll
-                for (int i = 0; i < 3; ++i) L2[i] += t3[i];
-                cross3(Sk, hc[ck], t3);
-#pragma unroll
-                for (int i = 0; i < 3; ++i) P2[i] = mc[ck] * Sk[3 + i] + t3[i];
-                Mp[tri<0>(l, k)] = dot3(Sl, L2) + dot3(Sl + 3, P2);
-            } else {
-                Mp[tri<0>(l, k)] = 0;
-            }
-        });
-    });
+}
+
+/* symmetric 3x3 (xx yy zz xy xz yz) times v */
+template <typename Real> DEV void symv(const Real *J, const Real *v, Real *o) {
+    Real x = J[0] * v[0] + J[3] * v[1] + J[4] * v[2];
+    Real y = J[3] * v[0] + J[1] * v[1] + J[5] * v[2];
+    Real z = J[4] * v[0] + J[5] * v[1] + J[2] * v[2];
+    o[0] = x; o[1] = y; o[2] = z;
 }
 
 /* in-place packed-lower Cholesky solve; returns false if not SPD */
@@ -569,106 +576,108 @@ template <typename Real> DEV Real smooth_step_d(Real y0, Real y1, Real x0, Real 
     return (y1 - y0) * Real(30) * t * t * (Real(1) - t) * (Real(1) - t) / w;
 }
 
-template <class T, typename Real> struct Contact {
-    Real F[T::NF > 0 ? T::NF : 1][3], Mo[T::NF > 0 ? T::NF : 1][3];
-};
-
-/* Hunt-Crossley spheres vs ground plane; h > 0 adds the implicit terms */
+/* Hunt-Crossley sphere s (this lane) vs the ground plane: publishes the
+ * generalized force, (h > 0) the implicit matrix contribution, and the
+ * sphere's wrench about the (shifted) ground origin. */
 template <class T, typename Real>
-DEV void contact_all(const DModel<Real> &M, const Work<T, Real> &W, Real *tau, Real *Mp, Real h, Contact<T, Real> &co) {
-    sfor<0, T::NF>([&](auto fI) {
-        constexpr int f = decltype(fI)::value;
+DEV void contact_lane(const DModel<Real> &M, const Real (&S)[Lay<T, Real>::ND][6], Real *lds, int s, Real h) {
+    using LY = Lay<T, Real>;
+    constexpr int ND = LY::ND;
+    const int cb = M.sph_cb[s], fo = M.sph_force[s];
+    const uint32_t mask = M.dofmask[cb];
+    const Real *kb = lds + LY::KB + 18 * cb;
+    Real *cw = lds + LY::CW + 8 * s;
+    Real *ct = lds + LY::CT + ND * s;
+    Real Cn[3];
+    mv3(kb, M.sph_loc[s], Cn);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) { co.F[f][i] = 0; co.Mo[f][i] = 0; }
+    for (int i = 0; i < 3; ++i) Cn[i] += kb[9 + i];
+    Real rad = M.sph_r[s];
+    Real depth = rad - Cn[1];
+    Real fn = 0, fH = 0, vn = 0, P[3] = {0, 0, 0}, vs[3] = {0, 0, 0};
+    if (depth > 0) {
+        P[0] = Cn[0]; P[1] = Cn[1] - (rad - Real(0.5) * depth); P[2] = Cn[2];
+        Real t[3];
+        cross3(kb + 12, P, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) vs[i] = kb[15 + i] + t[i];
+        vn = -vs[1];
+        Real kk = M.cf_kk[fo];
+        fH = Real(4.0 / 3.0) * kk * depth * sqrt(rad * kk * depth);
+        fn = fH * (Real(1) + Real(1.5) * M.cf_c[fo] * vn);
+    }
+    bool active = fn > 0;
+    cw[6] = active ? Real(1) : Real(0);
+    if (!active) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) cw[i] = 0;
+        return;
+    }
+    Real F[3] = {0, fn, 0};
+    Real vt0 = -vs[0], vt2 = -vs[2];
+    Real vslip = sqrt(vt0 * vt0 + vt2 * vt2);
+    Real vtr = M.cf_vt[fo], ms = M.cf_ms[fo], md = M.cf_md[fo], mv = M.cf_mv[fo];
+    Real r_ = vslip / vtr, den = Real(1) + r_ * r_;
+    if (vslip != 0) {
+        Real ff = fn * (fmin(r_, Real(1)) * (md + Real(2) * (ms - md) / den) + mv * vslip);
+        F[0] += ff * vt0 / vslip;
+        F[2] += ff * vt2 / vslip;
+    }
+    Real mo[3];
+    cross3(P, F, mo);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { cw[i] = F[i]; cw[3 + i] = mo[i]; }
+    Real kn = Real(1.5) * fH / depth * (Real(1) + Real(1.5) * M.cf_c[fo] * vn);
+    /* implicit extra force -h*Kn*v_y (Hertz force at the advanced position) */
+    Real Fy = F[1] - (h > 0 ? h * kn * vs[1] : Real(0));
+    Real Ft[3] = {F[0], Fy, F[2]}, mt[3];
+    cross3(P, Ft, mt);
+    Real jc[ND][3];
+    sfor<0, T::ND>([&](auto dI) {
+        constexpr int d = decltype(dI)::value;
+        Real on = (mask >> d) & 1u ? Real(1) : Real(0);
+        cross3(S[d], P, jc[d]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) jc[d][i] = on * (jc[d][i] + S[d][3 + i]);
+        ct[d] = on * (dot3(S[d], mt) + dot3(S[d] + 3, Ft));
     });
-    sfor<0, T::NS>([&](auto sI) {
-        constexpr int s = decltype(sI)::value;
-        constexpr int cb = T::sphere_cb[s];
-        constexpr int fo = T::sphere_force[s];
-        const Kin<Real> &k = W.K[cb];
-        Real Cn[3];
-        mv3(k.R, M.sph_loc[s], Cn);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) Cn[i] += k.o[i];
-        Real rad = M.sph_r[s];
-        Real depth = rad - Cn[1];
-        if (depth > 0) {
-            Real P[3] = {Cn[0], Cn[1] - (rad - Real(0.5) * depth), Cn[2]};
-            Real vs[3];
-            point_vel(k, P, vs);
-            Real vn = -vs[1];
-            Real kk = M.cf_kk[fo], cdis = M.cf_c[fo];
-            Real fH = Real(4.0 / 3.0) * kk * depth * sqrt(rad * kk * depth);
-            Real fn = fH * (Real(1) + Real(1.5) * cdis * vn);
-            if (fn > 0) {
-                Real F[3] = {0, fn, 0};
-                Real vt0 = -vs[0], vt2 = -vs[2];
-                Real vslip = sqrt(vt0 * vt0 + vt2 * vt2);
-                Real vtr = M.cf_vt[fo], ms = M.cf_ms[fo], md = M.cf_md[fo], mv = M.cf_mv[fo];
-                Real r_ = vslip / vtr, den = Real(1) + r_ * r_;
-                if (vslip != 0) {
-                    Real ff = fn * (fmin(r_, Real(1)) * (md + Real(2) * (ms - md) / den) + mv * vslip);
-                    F[0] += ff * vt0 / vslip;
-                    F[2] += ff * vt2 / vslip;
-                }
-                point_force<T, cb>(W, P, F, tau);
-                Real mo[3];
-                cross3(P, F, mo);
-#pragma unroll
-                for (int i = 0; i < 3; ++i) { co.F[fo][i] += F[i]; co.Mo[fo][i] += mo[i]; }
-                if (h > 0) {
-                    Real g_s, gp;
-                    if (r_ < 1) {
-                        g_s = (md + Real(2) * (ms - md) / den) / vtr + mv;
-                        gp = (md + Real(2) * (ms - md) / den) / vtr - Real(4) * (ms - md) * r_ * r_ / (den * den * vtr) + mv;
-                    } else {
-                        g_s = (md + Real(2) * (ms - md) / den) / vslip + mv;
-                        gp = -Real(4) * (ms - md) * r_ / (den * den * vtr) + mv;
-                    }
-                    gp = gp < 0 ? Real(0) : gp;
-                    Real tx = 0, tz = 0;
-                    if (vslip > 0) { tx = vt0 / vslip; tz = vt2 / vslip; }
-                    Real ct = h * fn * g_s, cq = h * fn * (gp - g_s);
-                    Real kn = Real(1.5) * fH / depth * (Real(1) + Real(1.5) * cdis * vn);
-                    Real cnn = h * Real(1.5) * cdis * fH + h * h * kn;
-                    Real C3[9] = {ct + cq * tx * tx, 0, cq * tx * tz, 0, cnn, 0, cq * tx * tz, 0, ct + cq * tz * tz};
-                    /* point Jacobian columns */
-                    Real jc[T::ND][3];
-                    sfor<0, T::ND>([&](auto dI) {
-                        constexpr int d = decltype(dI)::value;
-                        if constexpr ((T::dofmask[cb] >> d) & 1u) {
-                            cross3(W.S[d], P, jc[d]);
-#pragma unroll
-                            for (int i = 0; i < 3; ++i) jc[d][i] += W.S[d][3 + i];
-                        }
-                    });
-                    sfor<0, T::ND>([&](auto lI) {
-                        constexpr int l = decltype(lI)::value;
-                        if constexpr ((T::dofmask[cb] >> l) & 1u) {
-                            Real cj[3];
-                            mv3(C3, jc[l], cj);
-                            sfor<0, l + 1>([&](auto kI) {
-                                constexpr int kk2 = decltype(kI)::value;
-                                if constexpr ((T::dofmask[cb] >> kk2) & 1u) Mp[tri<0>(l, kk2)] += dot3(jc[kk2], cj);
-                            });
-                        }
-                    });
-                    Real Fk[3] = {0, -h * kn * vs[1], 0};
-                    point_force<T, cb>(W, P, Fk, tau);
-                }
-            }
+    if (h > 0) {
+        Real g_s, gp;
+        if (r_ < 1) {
+            g_s = (md + Real(2) * (ms - md) / den) / vtr + mv;
+            gp = (md + Real(2) * (ms - md) / den) / vtr - Real(4) * (ms - md) * r_ * r_ / (den * den * vtr) + mv;
+        } else {
+            g_s = (md + Real(2) * (ms - md) / den) / vslip + mv;
+            gp = -Real(4) * (ms - md) * r_ / (den * den * vtr) + mv;
         }
-    });
+        gp = gp < 0 ? Real(0) : gp;
+        Real tx = 0, tz = 0;
+        if (vslip > 0) { tx = vt0 / vslip; tz = vt2 / vslip; }
+        Real ctt = h * fn * g_s, cq = h * fn * (gp - g_s);
+        Real cnn = h * Real(1.5) * M.cf_c[fo] * fH + h * h * kn;
+        Real C3[9] = {ctt + cq * tx * tx, 0, cq * tx * tz, 0, cnn, 0, cq * tx * tz, 0, ctt + cq * tz * tz};
+        Real *cm = lds + LY::CM + LY::NP * s;
+        sfor<0, T::ND>([&](auto lI) {
+            constexpr int l = decltype(lI)::value;
+            Real cj[3];
+            mv3(C3, jc[l], cj);
+            sfor<0, l + 1>([&](auto kI) {
+                constexpr int k2 = decltype(kI)::value;
+                cm[tri<0>(l, k2)] = dot3(jc[k2], cj);
+            });
+        });
+    }
 }
 
 /* ------------------------------------------------------------ muscles */
 template <typename Real> struct MState {
-    Real act, lce, vce, Ft, Ff, Fa, dadt, dvdl;
+    Real act, lce, vN, vce, Ft, Ff, Fa, dadt, dvdl;
     bool clamped;
 };
 
 template <typename Real>
-DEV void muscle_eval(const DMuscle<Real> &mu, Real a_state, Real l_state, Real excitation, Real L, MState<Real> &s) {
+DEV void muscle_eval(const DMuscle<Real> &mu, Real a_state, Real l_state, Real excitation, Real L, Real v_warm,
+                     MState<Real> &s) {
     Real a = a_state < mu.amin ? mu.amin : (a_state > Real(1) ? Real(1) : a_state);
     Real lce = l_state < mu.lmin ? mu.lmin : l_state;
     Real w = mu.width;
@@ -681,7 +690,7 @@ DEV void muscle_eval(const DMuscle<Real> &mu, Real a_state, Real l_state, Real e
     curve_eval(mu.fpe, lce * mu.inv_lopt, fpe, dfpe);
     Real rhs = fse / cosphi - fpe;
     Real vN, fvv, dfv;
-    solve_fv(mu.fv, a * fal, mu.beta, rhs, vN, fvv, dfv);
+    solve_fv(mu.fv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
     Real dGdv = a * fal * dfv + mu.beta;
     bool clamped = (l_state <= mu.lmin && vN <= 0) || l_state < mu.lmin;
     if (clamped) {
@@ -692,6 +701,7 @@ DEV void muscle_eval(const DMuscle<Real> &mu, Real a_state, Real l_state, Real e
     }
     s.act = a;
     s.lce = lce;
+    s.vN = vN;
     s.vce = vN * mu.lv;
     s.Ft = mu.fiso * fse;
     s.Fa = mu.fiso * a * fal * fvv;
@@ -738,12 +748,13 @@ DEV Real muscle_equilibrium(const DMuscle<Real> &mu, Real a_state, Real L) {
     return l;
 }
 
-/* path length, moment arms dL/dq for the muscle of this lane (body frames
- * and coordinates from LDS, Plucker columns from registers) */
+/* path length and dL/dq of muscle m (frames from LDS, Plucker columns in registers) */
 template <class T, typename Real>
-DEV void muscle_path(const DModel<Real> &M, const Work<T, Real> &W, const Real *ldsR, const Real *ldsq, int m,
-                     Real &L, Real *dLdq) {
+DEV void muscle_path(const DModel<Real> &M, const Real (&S)[Lay<T, Real>::ND][6], const Real *lds, int m, Real &L,
+                     Real *dLdq) {
+    using LY = Lay<T, Real>;
     const DMuscle<Real> &mu = M.mus[m];
+    const Real *ldsq = lds + LY::QF;
     L = 0;
 #pragma unroll
     for (int d = 0; d < T::ND; ++d) dLdq[d] = 0;
@@ -751,6 +762,15 @@ DEV void muscle_path(const DModel<Real> &M, const Work<T, Real> &W, const Real *
     uint32_t maskp = 0;
     int mdofp = -1;
     bool have = false;
+    auto flush = [&](const Real *g) {
+        Real mo[3];
+        cross3(Pp, g, mo);
+        sfor<0, T::ND>([&](auto dI) {
+            constexpr int d = decltype(dI)::value;
+            Real on = (maskp >> d) & 1u ? Real(1) : Real(0);
+            dLdq[d] += on * (dot3(S[d], mo) + dot3(S[d] + 3, g)) + (mdofp == d ? dot3(g, dPp) : Real(0));
+        });
+    };
     for (int j = 0; j < mu.npt; ++j) {
         const DPathPt<Real> &pt = M.pt[mu.pt_off + j];
         if (pt.type == BIOIM_PT_COND) {
@@ -775,7 +795,7 @@ DEV void muscle_path(const DModel<Real> &M, const Work<T, Real> &W, const Real *
 #pragma unroll
             for (int i = 0; i < 3; ++i) loc[i] = pt.loc[i];
         }
-        const Real *Rb = ldsR + 12 * pt.cbody;
+        const Real *Rb = lds + LY::KB + 18 * pt.cbody;
         Real P[3], dP[3];
         mv3(Rb, loc, P);
 #pragma unroll
@@ -789,14 +809,8 @@ DEV void muscle_path(const DModel<Real> &M, const Work<T, Real> &W, const Real *
             Real inv = Real(1) / len;
 #pragma unroll
             for (int a = 0; a < 3; ++a) e[a] = sgm[a] * inv;
-            /* previous point is now complete: g = e_prev_prev - e */
-            Real g[3] = {ep[0] - e[0], ep[1] - e[1], ep[2] - e[2]}, mo[3];
-            cross3(Pp, g, mo);
-            sfor<0, T::ND>([&](auto dI) {
-                constexpr int d = decltype(dI)::value;
-                Real on = (maskp >> d) & 1u ? Real(1) : Real(0);
-                dLdq[d] += on * (dot3(W.S[d], mo) + dot3(W.S[d] + 3, g)) + (mdofp == d ? dot3(g, dPp) : Real(0));
-            });
+            Real g[3] = {ep[0] - e[0], ep[1] - e[1], ep[2] - e[2]};
+            flush(g);
         }
 #pragma unroll
         for (int a = 0; a < 3; ++a) { ep[a] = e[a]; Pp[a] = P[a]; dPp[a] = dP[a]; }
@@ -804,134 +818,192 @@ DEV void muscle_path(const DModel<Real> &M, const Work<T, Real> &W, const Real *
         mdofp = pt.mdof;
         have = true;
     }
-    if (have) { /* last point: g = e_prev */
-        Real g[3] = {ep[0], ep[1], ep[2]}, mo[3];
-        cross3(Pp, g, mo);
-        sfor<0, T::ND>([&](auto dI) {
-            constexpr int d = decltype(dI)::value;
-            Real on = (maskp >> d) & 1u ? Real(1) : Real(0);
-            dLdq[d] += on * (dot3(W.S[d], mo) + dot3(W.S[d] + 3, g)) + (mdofp == d ? dot3(g, dPp) : Real(0));
-        });
-    }
+    if (have) flush(ep);
 }
 
-/* -------------------------------------------------------- env context */
-template <class T, typename Real> struct Lds {
-    static constexpr int BODY = 12 * T::NB;     /* R, o per composite */
-    static constexpr int Q = BODY;              /* qf[NC]             */
-    static constexpr int OBS = ((Q + T::NC + 3) / 4) * 4;
-    static constexpr int SIZE = OBS + BIOIM_OBS_MAX;
-};
-
+/* ------------------------------------------------------------ dynamics */
 template <class T, typename Real> struct Dyn {
-    Real qdd[T::ND];
-    MState<Real> ms;             /* this lane's muscle */
-    Contact<T, Real> co;
-    Real limf[T::NL > 0 ? T::NL : 1];
+    Real qdd[Lay<T, Real>::ND];
+    MState<Real> ms; /* this lane's muscle */
+    Real act, lce;   /* this lane's muscle state used (after a reset equilibrium) */
+    Real x0;         /* floating origin used for the published frames */
     bool ok;
 };
 
-/* full dynamics at (q, u, lane muscle state) with controls; h > 0 gives the
- * implicit-step increment, h == 0 the true accelerations */
+/* Forward dynamics at (q, u, this lane's muscle state) with held controls.
+ * h > 0: increment of the linearly-implicit substep; h == 0: the true
+ * accelerations (realize).  Leaves frames, contact wrenches and limit
+ * forces published in LDS for reporting. */
 template <class T, typename Real>
-DEV void dynamics(const DModel<Real> &M, Work<T, Real> &W, const Real *q, const Real *u, Real act, Real lce,
-                  Real control, int lane, Real *lds, Real h, Dyn<T, Real> &D) {
-    constexpr int ND = T::ND;
-    fill_coords<T, Real>(M, q, u, W);
-    kinematics<T, Real>(M, W);
-    if constexpr (T::NM > 0) {
-        /* stage composite frames + coordinates for the muscle lanes */
-        if (lane == 0) {
-            sfor<0, T::NB>([&](auto cI) {
-                constexpr int c = decltype(cI)::value;
+DEV void dynamics(const DModel<Real> &M, const Real *q, const Real *u, Real act, Real lce, Real control, int lane,
+                  Real *lds, Real h, bool equilibrate, Dyn<T, Real> &D) {
+    using LY = Lay<T, Real>;
+    constexpr int ND = LY::ND, NP = LY::NP, NB = T::NB, G = T::G;
+    STAMP_DECL
+    Real qf[T::NC], uf[T::NC];
+    fill_coords<T, Real>(M, q, u, qf, uf);
+    Real x0 = 0;
+    if constexpr (T::TX >= 0) x0 = M.float_origin ? qf[T::TX] : Real(0);
+    D.x0 = x0;
+    Real S[ND][6];
+    const bool pub = (lane == 0);
+    if (pub) {
 #pragma unroll
-                for (int i = 0; i < 9; ++i) lds[12 * c + i] = W.K[c].R[i];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) lds[12 * c + 9 + i] = W.K[c].o[i];
-            });
-#pragma unroll
-            for (int c = 0; c < T::NC; ++c) lds[Lds<T, Real>::Q + c] = W.qf[c];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int c = 0; c < T::NC; ++c) lds[LY::QF + c] = qf[c];
     }
-    Real Mp[Work<T, Real>::NP], bias[ND], tau[ND];
-    mass_bias<T, Real>(M, W, Mp, bias);
+    kinematics<T, Real>(M, qf, uf, x0, S, lds, pub);
+    wave_sync();
+    STAMP(0);
+
+    /* ---- phase 2: lane-parallel force elements */
+    if (lane < NB) { /* subtree sums of inertia and wrench */
+        Real ic[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, wb[6] = {0, 0, 0, 0, 0, 0};
+        sfor<0, NB>([&](auto dI) {
+            constexpr int d = decltype(dI)::value;
+            if ((T::anc[d] >> lane) & 1u) {
 #pragma unroll
-    for (int d = 0; d < ND; ++d) tau[d] = 0;
-    if constexpr (T::NM > 0) {
-        Real dLdq[ND];
-        Real L = 0;
-        if (lane < T::NM) {
-            muscle_path<T, Real>(M, W, lds, lds + Lds<T, Real>::Q, lane, L, dLdq);
-            muscle_eval(M.mus[lane], act, lce, control, L, D.ms);
+                for (int i = 0; i < 10; ++i) ic[i] += lds[LY::IC + 10 * d + i];
 #pragma unroll
-            for (int d = 0; d < ND; ++d) tau[d] = -D.ms.Ft * dLdq[d];
-        }
-#pragma unroll
-        for (int d = 0; d < ND; ++d) tau[d] = group_sum<T::G>(tau[d]);
-        __builtin_amdgcn_wave_barrier();
-    } else {
-        /* coordinate actuators: action entry i acts on dof act_dof[i] */
-        sfor<0, T::NA>([&](auto iI) {
-            constexpr int i = decltype(iI)::value;
-            constexpr int d = T::act_dof[i];
-            if constexpr (d >= 0) {
-                Real ci = __shfl(control, ((threadIdx.x & 63) & ~(T::G - 1)) + i, 64);
-                tau[d] += ci * M.ca_opt[i];
+                for (int i = 0; i < 6; ++i) wb[i] += lds[LY::WB + 6 * d + i];
             }
         });
+#pragma unroll
+        for (int i = 0; i < 10; ++i) lds[LY::ICS + 10 * lane + i] = ic[i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) lds[LY::WBS + 6 * lane + i] = wb[i];
     }
-    Real *Meff = Mp;
-    contact_all<T, Real>(M, W, tau, Meff, h, D.co);
-    sfor<0, T::NL>([&](auto lI) {
-        constexpr int l = decltype(lI)::value;
-        constexpr int d = T::limit_dof[l];
-        constexpr int cc = T::limit_coord[l];
-        Real qv = W.qf[cc], qd = W.uf[cc];
-        Real qup = M.lim_qup[l], qlo = M.lim_qlow[l], tr = M.lim_trans[l];
+    STAMP(1);
+    if constexpr (T::NM > 0) {
+        if (lane < T::NM) {
+            Real L, dLdq[ND];
+            muscle_path<T, Real>(M, S, lds, lane, L, dLdq);
+            if (equilibrate) { /* reset: default activation, static fiber equilibrium */
+                act = M.mus[lane].default_act;
+                lce = muscle_equilibrium(M.mus[lane], act, L);
+            }
+            D.act = act;
+            D.lce = lce;
+            muscle_eval(M.mus[lane], act, lce, control, L, D.ms.vN, D.ms);
+#pragma unroll
+            for (int d = 0; d < ND; ++d) lds[LY::TAU + ND * lane + d] = -D.ms.Ft * dLdq[d];
+        }
+    } else {
+        if (lane < T::NA) {
+            int ad = M.act_dof[lane];
+            Real f = control * M.ca_opt[lane];
+#pragma unroll
+            for (int d = 0; d < ND; ++d) lds[LY::TAU + ND * lane + d] = (d == ad) ? f : Real(0);
+        }
+    }
+    STAMP(2);
+    if (lane < T::NS) contact_lane<T, Real>(M, S, lds, lane, h);
+    STAMP(3);
+    if (lane < T::NL) {
+        int cc = M.lim_coord[lane];
+        Real qv = lds[LY::QF + cc], qd = uf[0];
+#pragma unroll
+        for (int c = 1; c < T::NC; ++c) qd = (c == cc) ? uf[c] : qd;
+        Real qup = M.lim_qup[lane], qlo = M.lim_qlow[lane], tr = M.lim_trans[lane];
         Real up = smooth_step(Real(0), Real(1), qup, qup + tr, qv);
         Real lo = smooth_step(Real(1), Real(0), qlo - tr, qlo, qv);
-        Real f = -M.lim_kup[l] * up * (qv - qup) + M.lim_klow[l] * lo * (qlo - qv) - M.lim_damp[l] * (up + lo) * qd;
-        D.limf[l] = f;
-        if constexpr (d >= 0) {
-            tau[d] += f;
-            if (h > 0) {
-                Real dup = smooth_step_d(Real(0), Real(1), qup, qup + tr, qv);
-                Real dlo = smooth_step_d(Real(1), Real(0), qlo - tr, qlo, qv);
-                Real kq = M.lim_kup[l] * (up + dup * (qv - qup)) + M.lim_klow[l] * (lo - dlo * (qlo - qv));
-                Real cq = M.lim_damp[l] * (up + lo);
-                Meff[tri<0>(d, d)] += h * cq + h * h * kq;
-                tau[d] -= h * kq * qd;
-            }
+        Real f = -M.lim_kup[lane] * up * (qv - qup) + M.lim_klow[lane] * lo * (qlo - qv) - M.lim_damp[lane] * (up + lo) * qd;
+        Real diag = 0, tadd = f;
+        if (h > 0) {
+            Real dup = smooth_step_d(Real(0), Real(1), qup, qup + tr, qv);
+            Real dlo = smooth_step_d(Real(1), Real(0), qlo - tr, qlo, qv);
+            Real kq = M.lim_kup[lane] * (up + dup * (qv - qup)) + M.lim_klow[lane] * (lo - dlo * (qlo - qv));
+            Real cq = M.lim_damp[lane] * (up + lo);
+            diag = h * cq + h * h * kq;
+            tadd = f - h * kq * qd;
         }
-    });
+        Real *lm = lds + LY::LIM + 4 * lane;
+        lm[0] = f; lm[1] = diag; lm[2] = tadd;
+    }
+    wave_sync();
+    STAMP(4);
+
+    /* ---- phase 3: mass-matrix entries and right-hand side, fixed-order sums */
+    for (int e = lane; e < NP; e += G) {
+        int l = M.e_l[e], k = M.e_k[e], c = M.e_c[e];
+        Real v = 0;
+        if (c >= 0) {
+            const Real *Sl = lds + LY::S + 6 * l, *Sk = lds + LY::S + 6 * k, *ic = lds + LY::ICS + 10 * c;
+            Real Lm[3], Pm[3], t[3];
+            symv(ic + 4, Sl, Lm);
+            cross3(ic + 1, Sl + 3, t);
 #pragma unroll
-    for (int d = 0; d < ND; ++d) D.qdd[d] = tau[d] - bias[d];
-    D.ok = cholesky_solve<ND, Real>(Meff, D.qdd);
+            for (int i = 0; i < 3; ++i) Lm[i] += t[i];
+            cross3(Sl, ic + 1, t);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) Pm[i] = ic[0] * Sl[3 + i] + t[i];
+            v = dot3(Sk, Lm) + dot3(Sk + 3, Pm);
+        }
+        if (h > 0) {
+#pragma unroll
+            for (int s = 0; s < T::NS; ++s)
+                if (lds[LY::CW + 8 * s + 6] > 0) v += lds[LY::CM + NP * s + e];
+            if (l == k)
+#pragma unroll
+                for (int li = 0; li < T::NL; ++li)
+                    if (M.lim_dof[li] == l) v += lds[LY::LIM + 4 * li + 1];
+        }
+        lds[LY::MP + e] = v;
+    }
+    if (lane < ND) {
+        const Real *Sd = lds + LY::S + 6 * lane, *wb = lds + LY::WBS + 6 * M.dof_cb[lane];
+        Real r = -(dot3(Sd, wb) + dot3(Sd + 3, wb + 3));
+#pragma unroll
+        for (int m = 0; m < LY::NMS; ++m)
+            if (m < (T::NM > 0 ? T::NM : T::NA)) r += lds[LY::TAU + ND * m + lane];
+#pragma unroll
+        for (int s = 0; s < T::NS; ++s)
+            if (lds[LY::CW + 8 * s + 6] > 0) r += lds[LY::CT + ND * s + lane];
+#pragma unroll
+        for (int li = 0; li < T::NL; ++li)
+            if (M.lim_dof[li] == lane) r += lds[LY::LIM + 4 * li + 2];
+        lds[LY::RHS + lane] = r;
+    }
+    wave_sync();
+    STAMP(5);
+
+    /* ---- phase 4: redundant Cholesky solve in registers */
+    Real A[NP];
+#pragma unroll
+    for (int e = 0; e < NP; ++e) A[e] = lds[LY::MP + e];
+#pragma unroll
+    for (int d = 0; d < ND; ++d) D.qdd[d] = lds[LY::RHS + d];
+    D.ok = cholesky_solve<ND, Real>(A, D.qdd);
+    wave_sync();
+    STAMP(6);
 }
 
-/* body origin (OpenSim body ob) / system COM (ob = -1) */
+/* body origin position/velocity of OpenSim body OB (-1 = system COM), in
+ * absolute ground coordinates, from the published frames */
 template <class T, int OB, typename Real>
-DEV void report_body(const DModel<Real> &M, const Work<T, Real> &W, Real *pos, Real *vel) {
+DEV void report_body(const DModel<Real> &M, const Real *lds, Real x0, Real *pos, Real *vel) {
+    using LY = Lay<T, Real>;
     if constexpr (OB >= 0) {
         constexpr int c = T::os_cb[OB];
-        const Kin<Real> &k = W.K[c];
-        mv3(k.R, M.os_p[OB], pos);
+        const Real *kb = lds + LY::KB + 18 * c;
+        mv3(kb, M.os_p[OB], pos);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) pos[i] += k.o[i];
-        point_vel(k, pos, vel);
+        for (int i = 0; i < 3; ++i) pos[i] += kb[9 + i];
+        Real t[3];
+        cross3(kb + 12, pos, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) vel[i] = kb[15 + i] + t[i];
     } else {
         Real mt = 0, cs[3] = {0, 0, 0}, vs[3] = {0, 0, 0};
         sfor<0, T::NB>([&](auto cI) {
             constexpr int c = decltype(cI)::value;
-            const Kin<Real> &k = W.K[c];
-            Real cG[3], vc[3];
-            mv3(k.R, M.com[c], cG);
+            const Real *kb = lds + LY::KB + 18 * c;
+            Real cG[3], vc[3], t[3];
+            mv3(kb, M.com[c], cG);
 #pragma unroll
-            for (int i = 0; i < 3; ++i) cG[i] += k.o[i];
-            point_vel(k, cG, vc);
+            for (int i = 0; i < 3; ++i) cG[i] += kb[9 + i];
+            cross3(kb + 12, cG, t);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) vc[i] = kb[15 + i] + t[i];
             Real m = M.mass[c];
 #pragma unroll
             for (int i = 0; i < 3; ++i) { cs[i] += m * cG[i]; vs[i] += m * vc[i]; }
@@ -940,9 +1012,10 @@ DEV void report_body(const DModel<Real> &M, const Work<T, Real> &W, Real *pos, R
 #pragma unroll
         for (int i = 0; i < 3; ++i) { pos[i] = cs[i] / mt; vel[i] = vs[i] / mt; }
     }
+    pos[0] += x0;
 }
 
-template <int N> DEV int clamp_row(int r, int nrows) { return r < 0 ? 0 : (r >= nrows ? nrows - 1 : r); }
+DEV int clamp_row(int r, int nrows) { return r < 0 ? 0 : (r >= nrows ? nrows - 1 : r); }
 
 /* counter-based RNG (splitmix64) for device-drawn reset indices */
 DEV uint64_t splitmix64(uint64_t x) {
@@ -957,23 +1030,25 @@ DEV int draw_index(uint64_t seed, int env, int count, int hi) {
 }
 
 /* ---------------------------------------------------------------- kernel
- * mode 0: env step (optionally auto-reset); mode 1: reset listed envs */
+ * One 64-lane workgroup = 64/G envs.  mode 0: env step (optionally with
+ * in-kernel auto-reset); mode 1: reset the listed envs. */
 template <class T, typename Real>
-__global__ __launch_bounds__(256) void env_kernel(const DModel<Real> *__restrict__ Mg, DState<Real> st, int N, int mode,
-                                                  const Real *__restrict__ actions, Real *__restrict__ obs,
-                                                  Real *__restrict__ reward, uint8_t *__restrict__ done_out,
-                                                  Real *__restrict__ info, const int32_t *__restrict__ env_ids,
-                                                  const int32_t *__restrict__ ref_index, int n_list, int auto_reset,
-                                                  uint64_t seed) {
-    constexpr int G = T::G, ND = T::ND, NA = T::NA, NM = T::NM;
-    constexpr int ENVS_PER_BLOCK = 256 / G;
+__global__ __launch_bounds__(64) void env_kernel(const DModel<Real> *__restrict__ Mg, DState<Real> st, int N, int mode,
+                                                 const Real *__restrict__ actions, Real *__restrict__ obs,
+                                                 Real *__restrict__ reward, uint8_t *__restrict__ done_out,
+                                                 Real *__restrict__ info, const int32_t *__restrict__ env_ids,
+                                                 const int32_t *__restrict__ ref_index, int n_list, int auto_reset,
+                                                 uint64_t seed) {
+    using LY = Lay<T, Real>;
+    constexpr int G = T::G, ND = LY::ND, NA = T::NA, NM = T::NM;
+    constexpr int EPB = 64 / G;
     extern __shared__ __align__(16) unsigned char smem_raw[];
     Real *smem = reinterpret_cast<Real *>(smem_raw);
     const DModel<Real> &M = *Mg;
     const int lane = threadIdx.x % G;
     const int slot = threadIdx.x / G;
-    int gidx = blockIdx.x * ENVS_PER_BLOCK + slot;
-    Real *lds = smem + slot * Lds<T, Real>::SIZE;
+    int gidx = blockIdx.x * EPB + slot;
+    Real *lds = smem + slot * LY::SIZE;
     int env;
     if (mode == 1) {
         if (gidx >= n_list) return;
@@ -984,8 +1059,8 @@ __global__ __launch_bounds__(256) void env_kernel(const DModel<Real> *__restrict
         env = gidx;
     }
     const int H = M.horizon;
-    Work<T, Real> W;
     Dyn<T, Real> D;
+    D.ms.vN = 0;
     Real q[ND], u[ND];
 #pragma unroll
     for (int d = 0; d < ND; ++d) { q[d] = st.q[(size_t)d * N + env]; u[d] = st.u[(size_t)d * N + env]; }
@@ -1004,6 +1079,8 @@ __global__ __launch_bounds__(256) void env_kernel(const DModel<Real> *__restrict
     int reset_row = 0;
     if (mode == 1) reset_row = ref_index ? ref_index[gidx] : draw_index(seed, env, resets, M.reset_hi);
 
+    int remaining = 0;
+    Real dt = 0;
     if (mode == 0) {
         /* ---- action pre-processing (Env.step) */
         Real raw = lane < NA ? actions[(size_t)env * NA + lane] : Real(0);
@@ -1011,11 +1088,12 @@ __global__ __launch_bounds__(256) void env_kernel(const DModel<Real> *__restrict
         Real a = anynan ? Real(0) : raw;
         if constexpr ((T::FLAGS & BIOIM_ENV_PD) != 0) {
             if (!anynan) {
-                fill_coords<T, Real>(M, q, u, W);
+                Real qf[T::NC], uf[T::NC];
+                fill_coords<T, Real>(M, q, u, qf, uf);
                 Real xq = 0, xu = 0;
                 sfor<0, NA>([&](auto iI) {
                     constexpr int i = decltype(iI)::value;
-                    if (lane == i) { xq = W.qf[T::pd_coord[i]]; xu = W.uf[T::pd_coord[i]]; }
+                    if (lane == i) { xq = qf[T::pd_coord[i]]; xu = uf[T::pd_coord[i]]; }
                 });
                 if (lane < NA) a = M.kp[lane] * (raw - xq) - M.kv[lane] * xu;
             }
@@ -1036,33 +1114,26 @@ __global__ __launch_bounds__(256) void env_kernel(const DModel<Real> *__restrict
         Real hi = NM > 0 ? Real(1) : M.ca_max[lane < NA ? lane : 0];
         Real v = pnan ? Real(0) : phys;
         control = lane < NA ? (v < lo ? lo : (v > hi ? hi : v)) : Real(0);
-        /* ---- integrate to step_size * istep */
+        /* ---- integrate to step_size * istep (semi-implicit substeps) */
         istep += 1;
         double tf = M.step_size * (double)istep;
         double hstep = tf - t;
         if (hstep > 0) {
-            Real dt = Real(hstep / (double)M.nsub);
-            for (int s_ = 0; s_ < M.nsub; ++s_) {
-                dynamics<T, Real>(M, W, q, u, act, lce, control, lane, lds, dt, D);
-#pragma unroll
-                for (int d = 0; d < ND; ++d) { u[d] += dt * D.qdd[d]; q[d] += dt * u[d]; }
-                if (NM > 0 && lane < NM) {
-                    act += dt * D.ms.dadt;
-                    if (!D.ms.clamped) {
-                        Real ln = lce + dt * D.ms.vce / (Real(1) - dt * D.ms.dvdl);
-                        lce = ln < M.mus[lane].lmin ? M.mus[lane].lmin : ln;
-                    }
-                }
-            }
+            dt = Real(hstep / (double)M.nsub);
+            remaining = M.nsub;
         }
         t = tf;
     }
 
-    for (int pass = 0; pass < 2; ++pass) {
-        if (pass == 1 || do_reset) {
-            if (!do_reset) break;
-            /* ---- reset to reference row (Env.reset) */
-            int r = clamp_row<0>(reset_row, M.nrows);
+    /* One dynamics call site (inlined once): the substeps, then the realize
+     * at the end state; a reset (mode 1, or auto-reset after done) loads the
+     * reference row and folds the muscle fiber equilibrium into its realize. */
+    bool pending_reset = (mode == 1), reported_reset = false;
+    for (;;) {
+        const bool sub = remaining > 0;
+        const bool eq = !sub && pending_reset;
+        if (eq) {
+            int r = clamp_row(reset_row, M.nrows);
             sfor<0, T::NC>([&](auto cI) {
                 constexpr int c = decltype(cI)::value;
                 constexpr int d = T::coord_dof[c];
@@ -1073,60 +1144,63 @@ __global__ __launch_bounds__(256) void env_kernel(const DModel<Real> *__restrict
             has_last = 0;
             control = 0;
             resets += 1;
-            if constexpr (NM > 0) {
-                fill_coords<T, Real>(M, q, u, W);
-                kinematics<T, Real>(M, W);
-                if (lane == 0) {
-                    sfor<0, T::NB>([&](auto cI) {
-                        constexpr int c = decltype(cI)::value;
-#pragma unroll
-                        for (int i = 0; i < 9; ++i) lds[12 * c + i] = W.K[c].R[i];
-#pragma unroll
-                        for (int i = 0; i < 3; ++i) lds[12 * c + 9 + i] = W.K[c].o[i];
-                    });
-#pragma unroll
-                    for (int c = 0; c < T::NC; ++c) lds[Lds<T, Real>::Q + c] = W.qf[c];
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                if (lane < NM) {
-                    Real L, dLdq[ND];
-                    muscle_path<T, Real>(M, W, lds, lds + Lds<T, Real>::Q, lane, L, dLdq);
-                    act = M.mus[lane].default_act;
-                    lce = muscle_equilibrium(M.mus[lane], act, L);
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
         }
-        /* ---- realize at the current state */
-        dynamics<T, Real>(M, W, q, u, act, lce, control, lane, lds, Real(0), D);
-        Real *ob = lds + Lds<T, Real>::OBS;
+        {
+            /* opaque per-iteration model pointer: keeps the compiler from
+             * hoisting hundreds of loop-invariant constants into registers
+             * (they are re-read from the scalar cache instead of spilled) */
+            typedef const __attribute__((address_space(4))) DModel<Real> CModel;
+            CModel *Mi = (CModel *)Mg;
+            asm volatile("" : "+s"(Mi));
+            dynamics<T, Real>(*(const DModel<Real> *)Mi, q, u, act, lce, control, lane, lds, sub ? dt : Real(0),
+                              eq && NM > 0, D);
+        }
+        if (sub) {
+#pragma unroll
+            for (int d = 0; d < ND; ++d) { u[d] += dt * D.qdd[d]; q[d] += dt * u[d]; }
+            if (NM > 0 && lane < NM) {
+                act += dt * D.ms.dadt;
+                if (!D.ms.clamped) {
+                    Real ln = lce + dt * D.ms.vce / (Real(1) - dt * D.ms.dvdl);
+                    lce = ln < M.mus[lane].lmin ? M.mus[lane].lmin : ln;
+                }
+            }
+            --remaining;
+            continue;
+        }
+        if (eq) {
+            if (NM > 0 && lane < NM) { act = D.act; lce = D.lce; }
+            pending_reset = false;
+            reported_reset = true;
+        }
+        /* ---- realized state: observation */
+        const Real x0 = D.x0;
+        Real *ob = lds + LY::OBS;
         const bool tgt = (M.env_flags & BIOIM_ENV_TARGET_OBS) != 0, grf = (M.env_flags & BIOIM_ENV_GRF_OBS) != 0;
-        Real qdd_f[T::NC];
+        Real qdd_f[T::NC], qf[T::NC], uf[T::NC];
+        fill_coords<T, Real>(M, q, u, qf, uf);
         sfor<0, T::NC>([&](auto cI) {
             constexpr int c = decltype(cI)::value;
             constexpr int d = T::coord_dof[c];
             if constexpr (d >= 0) qdd_f[c] = D.qdd[d]; else qdd_f[c] = 0;
         });
-        Real px = W.qf[T::TX], py = W.qf[T::TY];
+        Real px = qf[T::TX], py = qf[T::TY];
         Real pz = 0;
-        if constexpr (T::TZ >= 0) pz = W.qf[T::TZ];
-        /* observation (get_state_dict + flatten), staged in LDS */
+        if constexpr (T::TZ >= 0) pz = qf[T::TZ];
         if (lane == 0) {
             int k = 0;
             double ph = (double)istep / (double)M.cycle;
             ob[k++] = Real(ph - floor(ph));
             sfor<0, T::NC>([&](auto cI) {
                 constexpr int c = decltype(cI)::value;
-                if constexpr (c != T::TX && c != T::TY && c != T::TZ) ob[k++] = W.qf[c];
+                if constexpr (c != T::TX && c != T::TY && c != T::TZ) ob[k++] = qf[c];
             });
 #pragma unroll
-            for (int c = 0; c < T::NC; ++c) ob[k++] = W.uf[c];
+            for (int c = 0; c < T::NC; ++c) ob[k++] = uf[c];
 #pragma unroll
             for (int c = 0; c < T::NC; ++c) ob[k++] = qdd_f[c];
             if (tgt) {
-                int r = clamp_row<0>(istep + 1, M.nrows);
+                int r = clamp_row(istep + 1, M.nrows);
 #pragma unroll
                 for (int c = 0; c < T::NC; ++c)
                     if (c != T::TX) ob[k++] = M.ref_q[r][c];
@@ -1137,23 +1211,35 @@ __global__ __launch_bounds__(256) void env_kernel(const DModel<Real> *__restrict
             sfor<0, T::NOBP>([&](auto bI) {
                 constexpr int b = decltype(bI)::value;
                 Real p3[3], v3[3];
-                report_body<T, T::obs_bpos[b], Real>(M, W, p3, v3);
+                report_body<T, T::obs_bpos[b], Real>(M, lds, x0, p3, v3);
                 ob[k++] = p3[0] - px; ob[k++] = p3[1] - py; ob[k++] = p3[2] - pz;
             });
             sfor<0, T::NOBV>([&](auto bI) {
                 constexpr int b = decltype(bI)::value;
                 Real p3[3], v3[3];
-                report_body<T, T::obs_bvel[b], Real>(M, W, p3, v3);
+                report_body<T, T::obs_bvel[b], Real>(M, lds, x0, p3, v3);
                 ob[k++] = v3[0]; ob[k++] = v3[1]; ob[k++] = v3[2];
             });
             k += 3 * NM;
             if (grf) {
                 sfor<0, T::NF>([&](auto fI) {
                     constexpr int f = decltype(fI)::value;
+                    Real F[3] = {0, 0, 0}, Mo[3] = {0, 0, 0};
+                    sfor<0, T::NS>([&](auto sI) {
+                        constexpr int s2 = decltype(sI)::value;
+                        if constexpr (T::sphere_force[s2] == f) {
+                            const Real *cw = lds + LY::CW + 8 * s2;
 #pragma unroll
-                    for (int i = 0; i < 3; ++i) ob[k++] = D.co.F[f][i] / M.weight;
+                            for (int i = 0; i < 3; ++i) { F[i] += cw[i]; Mo[i] += cw[3 + i]; }
+                        }
+                    });
+                    /* moments about the absolute ground origin: (x0,0,0) x F */
+                    Mo[1] += -x0 * F[2];
+                    Mo[2] += x0 * F[1];
 #pragma unroll
-                    for (int i = 0; i < 3; ++i) ob[k++] = D.co.Mo[f][i] / M.moment;
+                    for (int i = 0; i < 3; ++i) ob[k++] = F[i] / M.weight;
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) ob[k++] = Mo[i] / M.moment;
                 });
             }
         }
@@ -1166,21 +1252,19 @@ __global__ __launch_bounds__(256) void env_kernel(const DModel<Real> *__restrict
                 ob[mb + 3 * lane + 2] = D.ms.vce;
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_sync();
         if (obs)
             for (int k = lane; k < M.obs_dim; k += G) obs[(size_t)env * M.obs_dim + k] = ob[k];
-        __builtin_amdgcn_wave_barrier();
-        if (pass == 1 || mode == 1) break;
+        wave_sync();
+        if (reported_reset) break;
 
         /* ---- reward (get_reward) and termination (is_done) */
         {
-            int r = clamp_row<0>(istep, M.nrows);
+            int r = clamp_row(istep, M.nrows);
             Real qerr = 0;
 #pragma unroll
             for (int c = 0; c < T::NC; ++c) {
-                Real e = W.qf[c] - M.ref_q[r][c];
+                Real e = qf[c] - M.ref_q[r][c];
                 qerr += e * e;
             }
             qerr /= Real(T::NC);
@@ -1188,14 +1272,14 @@ __global__ __launch_bounds__(256) void env_kernel(const DModel<Real> *__restrict
             sfor<0, BIOIM_NREFBODY>([&](auto bI) {
                 constexpr int b = decltype(bI)::value;
                 Real p3[3], v3[3];
-                report_body<T, T::rw_body[b], Real>(M, W, p3, v3);
-                Real s = 0;
+                report_body<T, T::rw_body[b], Real>(M, lds, x0, p3, v3);
+                Real s2 = 0;
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
                     Real e = p3[i] - M.ref_x[r][b][i];
-                    s += e * e;
+                    s2 += e * e;
                 }
-                err[b] = s / Real(3);
+                err[b] = s2 / Real(3);
             });
             Real position_r = exp(Real(-30) * qerr);
             Real com_r = exp(Real(-20) * err[0]);
@@ -1238,9 +1322,10 @@ __global__ __launch_bounds__(256) void env_kernel(const DModel<Real> *__restrict
             old_px = pelvis_x;
             /* is_done */
             Real p3[3], v3[3];
-            report_body<T, T::TORSO, Real>(M, W, p3, v3);
+            report_body<T, T::TORSO, Real>(M, lds, x0, p3, v3);
             Real lmax = 0, amax = 0;
-            sfor<0, T::NL>([&](auto lI) { lmax = fmax(lmax, fabs(D.limf[decltype(lI)::value])); });
+#pragma unroll
+            for (int li = 0; li < T::NL; ++li) lmax = fmax(lmax, fabs(lds[LY::LIM + 4 * li]));
 #pragma unroll
             for (int c = 0; c < T::NC; ++c)
                 if (T::coord_dof[c] >= 0) amax = fmax(amax, fabs(qdd_f[c]));
@@ -1251,8 +1336,8 @@ __global__ __launch_bounds__(256) void env_kernel(const DModel<Real> *__restrict
             else if (istep >= M.n_episode) d_ = 1;
             else if constexpr ((T::FLAGS & BIOIM_ENV_DONE_CROSS) != 0) {
                 Real pr[3], pl[3];
-                report_body<T, T::CALCN_R, Real>(M, W, pr, v3);
-                report_body<T, T::CALCN_L, Real>(M, W, pl, v3);
+                report_body<T, T::CALCN_R, Real>(M, lds, x0, pr, v3);
+                report_body<T, T::CALCN_L, Real>(M, lds, x0, pl, v3);
                 if (pr[2] - pl[2] < 0) d_ = 1;
             }
 #pragma unroll
@@ -1271,12 +1356,14 @@ __global__ __launch_bounds__(256) void env_kernel(const DModel<Real> *__restrict
             for (int i = 1; i < 5; ++i) iv = lane == i ? inf[i] : iv;
             info[(size_t)env * M.info_dim + lane] = iv;
         }
+        wave_sync();
         if (done && auto_reset) {
+            pending_reset = true;
             do_reset = true;
             reset_row = draw_index(seed, env, resets, M.reset_hi);
-        } else {
-            break;
+            continue;
         }
+        break;
     }
 
     /* ---- store state */
@@ -1318,9 +1405,31 @@ int fail(int code, const std::string &msg) {
         if (e_ != hipSuccess) return fail(BIOIM_E_DEVICE, std::string(#x ": ") + hipGetErrorString(e_)); \
     } while (0)
 
+double host_bez5(const double *p, double u) {
+    double v = 1.0 - u;
+    return p[0] * v * v * v * v * v + 5 * p[1] * u * v * v * v * v + 10 * p[2] * u * u * v * v * v +
+           10 * p[3] * u * u * u * v * v + 5 * p[4] * u * u * u * u * v + p[5] * u * u * u * u * u;
+}
+
+/* exact inverse of the monotone quintic x(u) by bisection (host, table build) */
+double host_invert(const double *px, double x) {
+    double lo = 0.0, hi = 1.0;
+    for (int it = 0; it < 200; ++it) {
+        double m = 0.5 * (lo + hi);
+        if (host_bez5(px, m) > x) hi = m; else lo = m;
+    }
+    return 0.5 * (lo + hi);
+}
+
 template <typename Real> void convert_curve(const bioim_curve_t &s, DCurve<Real> &d) {
     for (int i = 0; i < BIOIM_MAX_CURVESEG; ++i)
         for (int j = 0; j < 6; ++j) { d.x[i][j] = (Real)s.x[i][j]; d.y[i][j] = (Real)s.y[i][j]; }
+    for (int k = 0; k < BIOIM_MAX_CURVESEG; ++k) {
+        if (k >= s.nseg) { d.inv_h[k] = 0; for (int i = 0; i <= BIOIM_UTAB; ++i) d.ut[k][i] = 0; continue; }
+        double a = s.x[k][0], b = s.x[k][5];
+        d.inv_h[k] = (Real)(BIOIM_UTAB / (b - a));
+        for (int i = 0; i <= BIOIM_UTAB; ++i) d.ut[k][i] = (Real)host_invert(s.x[k], a + (b - a) * i / BIOIM_UTAB);
+    }
     d.x0 = (Real)s.x0; d.y0 = (Real)s.y0; d.dydx0 = (Real)s.dydx0;
     d.x1 = (Real)s.x1; d.y1 = (Real)s.y1; d.dydx1 = (Real)s.dydx1;
     d.nseg = s.nseg;
@@ -1408,6 +1517,25 @@ template <typename Real> void convert_model(const bioim_modelpack_t &p, DModel<R
     m.moment = (Real)(wgt * p.height);
     m.torso_y_min = (Real)p.torso_y_min; m.limit_force_max = (Real)p.limit_force_max; m.acc_max = (Real)p.acc_max;
     for (int i = 0; i < 3; ++i) m.gravity[i] = (Real)p.gravity[i];
+    /* lane-parallel index tables */
+    m.float_origin = 1;
+    for (int c = 0; c < p.ncbody; ++c) {
+        uint32_t anc = 1u << c;
+        for (int q = p.cbody[c].parent; q >= 0; q = p.cbody[q].parent) anc |= 1u << q;
+        m.anc[c] = anc;
+        m.dofmask[c] = dofmask[c];
+    }
+    for (int c = 0; c < p.ncoord; ++c)
+        if (p.coord[c].dof >= 0) m.dof_cb[p.coord[c].dof] = p.coord[c].cbody;
+    for (int l = 0, e = 0; l < p.ndof; ++l)
+        for (int k = 0; k <= l; ++k, ++e) {
+            int cl = m.dof_cb[l], ck = m.dof_cb[k];
+            m.e_l[e] = l; m.e_k[e] = k;
+            m.e_c[e] = ((m.anc[cl] >> ck) & 1u) ? cl : (((m.anc[ck] >> cl) & 1u) ? ck : -1);
+        }
+    for (int s = 0; s < p.nsphere; ++s) { m.sph_cb[s] = p.sphere[s].cbody; m.sph_force[s] = p.sphere[s].force; }
+    for (int l = 0; l < p.nlimit; ++l) { m.lim_coord[l] = p.limit[l].coord; m.lim_dof[l] = p.limit[l].dof; }
+    for (int a = 0; a < p.ncoordact; ++a) m.act_dof[a] = p.coordact[a].dof;
     m.horizon = p.horizon; m.cycle = p.cycle; m.n_episode = p.n_episode; m.reset_hi = p.reset_hi;
     m.nsub = p.nsub; m.nrows = p.nrows; m.obs_dim = p.obs_dim; m.info_dim = p.info_dim; m.env_flags = p.env_flags;
     m.step_size = p.step_size;
@@ -1497,12 +1625,12 @@ namespace {
 template <class T, typename Real>
 void launch_impl(bioim_handle_t *h, int mode, const void *actions, void *obs, void *reward, uint8_t *done, void *info,
                  const int32_t *env_ids, const int32_t *ref_index, int n_list) {
-    constexpr int EPB = 256 / T::G;
+    constexpr int EPB = 64 / T::G;
     int count = mode == 1 ? n_list : h->n;
     int blocks = (count + EPB - 1) / EPB;
-    size_t lds = (size_t)EPB * Lds<T, Real>::SIZE * sizeof(Real);
+    size_t lds = (size_t)EPB * Lay<T, Real>::SIZE * sizeof(Real);
     DState<Real> st = *reinterpret_cast<DState<Real> *>(h->dstate);
-    hipLaunchKernelGGL((env_kernel<T, Real>), dim3(blocks), dim3(256), lds, h->stream,
+    hipLaunchKernelGGL((env_kernel<T, Real>), dim3(blocks), dim3(64), lds, h->stream,
                        reinterpret_cast<const DModel<Real> *>(h->model), st, h->n, mode,
                        reinterpret_cast<const Real *>(actions), reinterpret_cast<Real *>(obs),
                        reinterpret_cast<Real *>(reward), done, reinterpret_cast<Real *>(info), env_ids, ref_index,
@@ -1514,10 +1642,10 @@ template <class T> bool pick(const bioim_modelpack_t &p, int precision, Ops &ops
     ops.lanes = T::G;
     if (precision == 64) {
         ops.launch = &launch_impl<T, double>;
-        ops.lds_bytes_per_env = Lds<T, double>::SIZE * sizeof(double);
+        ops.lds_bytes_per_env = Lay<T, double>::SIZE * sizeof(double);
     } else {
         ops.launch = &launch_impl<T, float>;
-        ops.lds_bytes_per_env = Lds<T, float>::SIZE * sizeof(float);
+        ops.lds_bytes_per_env = Lay<T, float>::SIZE * sizeof(float);
     }
     return true;
 }
@@ -1735,6 +1863,18 @@ int bioim_set_stream(bioim_handle_t *h, void *s) {
     h->own_stream = false;
     return 0;
 }
+
+#ifdef BIOIM_STAMPS
+int bioim_debug_stamps(unsigned long long *out, int reset) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16));
+    if (reset) {
+        unsigned long long z[16] = {0};
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)));
+    }
+    return 0;
+}
+#endif
 
 int bioim_sync(bioim_handle_t *h) {
     if (!h) return fail(BIOIM_E_ARG, "null handle");

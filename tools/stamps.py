@@ -1,0 +1,34 @@
+"""Per-phase cycle shares of the dynamics substep (diagnostic build
+libbioim_stamps.so, -DBIOIM_STAMPS).  Read the shares, not absolute times."""
+import ctypes as C, os, sys
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ['BIOIM_LIB'] = os.path.join(REPO, 'bioimitation-gym_amd', 'build', 'libbioim_stamps.so')
+sys.path[:0] = [os.path.join(REPO, 'bioimitation-gym_amd')]
+import numpy as np, torch
+from bioimitation import _lib
+from bioimitation.vector_env import VectorEnv
+prec = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+env_id = sys.argv[2] if len(sys.argv) > 2 else 'MuscleWalkingImitation2D-v0'
+L = _lib.load()
+f = L.bioim_debug_stamps
+f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+env = VectorEnv(env_id, 4096, precision=prec, seed=1, auto_reset=True)
+env.reset()
+buf = (C.c_ulonglong * 16)()
+steps = 30
+acts = torch.rand((steps + 5, 4096, env.action_dim), device=env.device, dtype=env.dtype)
+for k in range(5):
+    env.step(acts[k])
+torch.cuda.synchronize()
+f(buf, 1)
+for k in range(steps):
+    env.step(acts[5 + k])
+torch.cuda.synchronize()
+f(buf, 1)
+names = ['kinematics(redundant)+publish', 'subtree sums', 'muscles/actuators', 'contacts', 'limits+sync',
+         'M entries + rhs', 'cholesky']
+tot = sum(buf[i] for i in range(7))
+calls = steps * (env.nsub + 1)
+print(f'{env_id} fp{prec}: cycles per dynamics call {tot / calls:.0f}')
+for i, n in enumerate(names):
+    print(f'  {n:32s} {buf[i] / calls:9.0f} cyc  {100.0 * buf[i] / tot:5.1f} %')
