@@ -18,8 +18,8 @@ from .registry import load_pack
 
 
 class VectorEnv:
-    def __init__(self, env_id: str, num_envs: int, config: dict = None, device: int = 0, precision: int = 32,
-                 seed: int = 0, auto_reset: bool = False):
+    def __init__(self, env_id: str, num_envs: int, config: dict = None, device: int = 0, precision: int = 64,
+                 seed: int = 0, auto_reset: bool = False, env_offset: int = 0):
         import torch
         if not torch.cuda.is_available():
             raise _lib.BioimError('VectorEnv needs a HIP GPU (no CPU fallback)')
@@ -41,6 +41,8 @@ class VectorEnv:
         self.obs_dim, self.action_dim, self.info_dim, self.lanes_per_env, self.nsub, self.state_dim = \
             q[1], q[2], q[3], q[5], q[6], q[7]
         _lib.check(L.bioim_set_auto_reset(h, 1 if auto_reset else 0))
+        _lib.check(L.bioim_set_env_offset(h, int(env_offset)))
+        self.env_offset = int(env_offset)
         n = self.num_envs
         self.obs = torch.zeros((n, self.obs_dim), dtype=self.dtype, device=self.device)
         self.reward = torch.zeros(n, dtype=self.dtype, device=self.device)

@@ -1038,7 +1038,7 @@ __global__ __launch_bounds__(64) void env_kernel(const DModel<Real> *__restrict_
                                                  Real *__restrict__ reward, uint8_t *__restrict__ done_out,
                                                  Real *__restrict__ info, const int32_t *__restrict__ env_ids,
                                                  const int32_t *__restrict__ ref_index, int n_list, int auto_reset,
-                                                 uint64_t seed) {
+                                                 uint64_t seed, int env_offset) {
     using LY = Lay<T, Real>;
     constexpr int G = T::G, ND = LY::ND, NA = T::NA, NM = T::NM;
     constexpr int EPB = 64 / G;
@@ -1077,7 +1077,7 @@ __global__ __launch_bounds__(64) void env_kernel(const DModel<Real> *__restrict_
     Real rew = 0, inf[5] = {0, 0, 0, 0, 0};
     bool do_reset = (mode == 1);
     int reset_row = 0;
-    if (mode == 1) reset_row = ref_index ? ref_index[gidx] : draw_index(seed, env, resets, M.reset_hi);
+    if (mode == 1) reset_row = ref_index ? ref_index[gidx] : draw_index(seed, env_offset + env, resets, M.reset_hi);
 
     int remaining = 0;
     Real dt = 0;
@@ -1360,7 +1360,7 @@ __global__ __launch_bounds__(64) void env_kernel(const DModel<Real> *__restrict_
         if (done && auto_reset) {
             pending_reset = true;
             do_reset = true;
-            reset_row = draw_index(seed, env, resets, M.reset_hi);
+            reset_row = draw_index(seed, env_offset + env, resets, M.reset_hi);
             continue;
         }
         break;
@@ -1608,7 +1608,7 @@ struct Ops {
 }  // namespace
 
 struct bioim_handle {
-    int n, device, precision, ndof, nmuscle, nact, horizon, obs_dim, info_dim, nsub, auto_reset;
+    int n, device, precision, ndof, nmuscle, nact, horizon, obs_dim, info_dim, nsub, auto_reset, env_offset;
     uint64_t seed;
     hipStream_t stream;
     bool own_stream;
@@ -1634,7 +1634,7 @@ void launch_impl(bioim_handle_t *h, int mode, const void *actions, void *obs, vo
                        reinterpret_cast<const DModel<Real> *>(h->model), st, h->n, mode,
                        reinterpret_cast<const Real *>(actions), reinterpret_cast<Real *>(obs),
                        reinterpret_cast<Real *>(reward), done, reinterpret_cast<Real *>(info), env_ids, ref_index,
-                       n_list, h->auto_reset, h->seed);
+                       n_list, h->auto_reset, h->seed, h->env_offset);
 }
 
 template <class T> bool pick(const bioim_modelpack_t &p, int precision, Ops &ops, std::vector<uint32_t> &dofmask) {
@@ -1776,6 +1776,7 @@ int bioim_create(const bioim_modelpack_t *pack, int n_envs, int device, int prec
     h->n = n_envs; h->device = device; h->precision = precision; h->seed = seed;
     h->ndof = pack->ndof; h->nmuscle = pack->nmuscle; h->nact = pack->nact; h->horizon = pack->horizon;
     h->obs_dim = pack->obs_dim; h->info_dim = pack->info_dim; h->nsub = pack->nsub; h->auto_reset = 0;
+    h->env_offset = 0;
     h->ops = ops;
     memcpy(&h->pack, pack, sizeof(bioim_modelpack_t));
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1824,6 +1825,12 @@ int bioim_step(bioim_handle_t *h, const void *actions, void *obs, void *reward, 
 int bioim_set_auto_reset(bioim_handle_t *h, int on) {
     if (!h) return fail(BIOIM_E_ARG, "null handle");
     h->auto_reset = on ? 1 : 0;
+    return 0;
+}
+
+int bioim_set_env_offset(bioim_handle_t *h, int offset) {
+    if (!h || offset < 0) return fail(BIOIM_E_ARG, "bioim_set_env_offset: bad arguments");
+    h->env_offset = offset;
     return 0;
 }
 

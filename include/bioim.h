@@ -81,6 +81,10 @@ int bioim_reset(bioim_handle_t *h, const int32_t *env_ids, const int32_t *ref_in
  * same launch and their obs row is the post-reset observation. */
 int bioim_step(bioim_handle_t *h, const void *actions, void *obs, void *reward, uint8_t *done, void *info);
 int bioim_set_auto_reset(bioim_handle_t *h, int on);
+/* Global index of this handle's env 0 (multi-GPU sharding): device-drawn
+ * reset indices depend on the global env index, so a sharded run is
+ * bit-identical to an unsharded one. */
+int bioim_set_env_offset(bioim_handle_t *h, int offset);
 
 /* Host-side state transfer (synchronous). */
 int bioim_state_dim(const bioim_handle_t *h);

@@ -1,0 +1,45 @@
+"""The device path inverts x(u) of each quintic Bezier segment with a
+32-interval u(x) table and exactly three Newton steps (bioim_step.hip
+curve_eval).  Verify that this scheme reaches machine precision on every
+segment of every curve of every built pack (host restatement of the scheme)."""
+import numpy as np
+
+from bioimitation import registry
+from bioimitation.curves import Curve
+
+B, dB = Curve._bern, Curve._dbern
+
+
+def _exact(px, x):
+    lo, hi = 0.0, 1.0
+    for _ in range(200):
+        m = 0.5 * (lo + hi)
+        if B(px, m) > x:
+            hi = m
+        else:
+            lo = m
+    return 0.5 * (lo + hi)
+
+
+def test_table_plus_three_newton_steps_converges():
+    worst = 0.0
+    for env_id in registry.RECIPES:
+        pk = registry.load_pack(env_id)
+        seen = set()
+        for m in range(pk.nmuscle):
+            for cv in (pk.muscle[m].fal, pk.muscle[m].fv, pk.muscle[m].fpe, pk.muscle[m].fse):
+                for s in range(cv.nseg):
+                    px = np.array(cv.x[s][:])
+                    if tuple(px) in seen:
+                        continue
+                    seen.add(tuple(px))
+                    a, b = px[0], px[5]
+                    ut = np.array([_exact(px, a + (b - a) * i / 32) for i in range(33)])
+                    xt = np.linspace(a, b, 997)
+                    tt = (xt - a) * (32 / (b - a))
+                    i0 = np.clip(tt.astype(int), 0, 31)
+                    u = ut[i0] + (tt - i0) * (ut[i0 + 1] - ut[i0])
+                    for _ in range(3):
+                        u = u - (B(px, u) - xt) / dB(px, u)
+                    worst = max(worst, np.abs(B(px, u) - xt).max())
+    assert worst < 5e-15, worst

@@ -1,0 +1,105 @@
+"""ModelPack compiler: layout agreement across the three consumers, model
+facts of the shipped 2D model, config patching, and the
+predictive-model transform against the reference's own shipped output."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from bioimitation import packdef as P
+from bioimitation.registry import load_pack
+
+REF_DATA = '/root/reference/bioimitation/imitation_envs/data'
+
+
+def test_pack_layout_matches_oracle(oracle_lib):
+    orc = oracle_lib.Oracle(load_pack('MuscleWalkingImitation2D-v0'))
+    assert orc.lib.orc_pack_size() == C.sizeof(P.ModelPack)
+
+
+def test_pack_layout_matches_product_library():
+    from bioimitation import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip('libbioim.so not built')
+    L = _lib.load()          # loads without a GPU; checks the size itself
+    assert L.bioim_modelpack_size() == C.sizeof(P.ModelPack)
+
+
+@pytest.mark.parametrize('env_id,obs,act,info', [('MuscleWalkingImitation2D-v0', 138, 14, 5),
+                                                 ('TorqueWalkingImitation2D-v0', 96, 7, 4)])
+def test_model_facts(env_id, obs, act, info):
+    pk = load_pack(env_id)
+    assert (pk.obs_dim, pk.nact, pk.info_dim) == (obs, act, info)
+    assert pk.ncoord == 9 and pk.ndof == 9 and pk.ncbody == 7 and pk.nosbody == 12
+    assert abs(pk.total_mass - 75.1646) < 1e-9
+    assert pk.nsphere == 6 and pk.ncforce == 2 and pk.nlimit == 6
+    assert pk.cycle == 132 and pk.n_episode == 264 and pk.reset_hi == 132
+    assert tuple(pk.gravity) == (0.0, -9.80665, 0.0)
+    # istep = int(t / 0.01) truncation quirk (opensim_wrapper.py:306): 16 of the first 364 rows
+    quirks = [r for r in range(pk.nrows) if pk.ref_istep[r] != r]
+    assert quirks[:7] == [29, 58, 59, 116, 117, 118, 119] and len(quirks) == 16
+
+
+def test_config_patching():
+    base = load_pack('MuscleWalkingImitation2D-v0')
+    pk = load_pack('MuscleWalkingImitation2D-v0', {'use_target_obs': False, 'use_GRF': False, 'horizon': 3,
+                                                   'r_weights': [0.5, 0.3, 0.2], 'mode': 'test'})
+    assert pk.obs_dim == base.obs_dim - 16 - 12
+    assert pk.horizon == 3 and abs(pk.w_imitate - 0.5) < 1e-15 and abs(pk.w_action - 0.2) < 1e-15
+    assert pk.n_episode == pk.nrows - 2 and pk.reset_hi == 0
+    with pytest.raises(ValueError):
+        load_pack('MuscleWalkingImitation2D-v0', {'horizon': 99})
+    with pytest.raises(NotImplementedError):
+        load_pack('MuscleJumpingImitation2D-v0')
+
+
+def test_spline_interpolates_knots_and_is_c2():
+    from bioimitation.splines import simm_spline_coeffs, simm_spline_eval
+    x = np.array([-2.0944, -1.22173, -0.523599, -0.349066, -0.174533, 0.159149, 2.0944])
+    y = np.array([-0.4226, -0.4082, -0.399, -0.3976, -0.3966, -0.395264, -0.396])
+    b, c, d = simm_spline_coeffs(x, y)
+    for i in range(len(x)):
+        assert abs(simm_spline_eval(x, y, b, c, d, x[i]) - y[i]) < 1e-14
+    for xi in x[1:-1]:
+        for k in (0, 1, 2):
+            lo = simm_spline_eval(x, y, b, c, d, xi - 1e-9, k)
+            hi = simm_spline_eval(x, y, b, c, d, xi + 1e-9, k)
+            assert abs(lo - hi) < 1e-6
+    # linear extrapolation with the end slopes
+    assert abs(simm_spline_eval(x, y, b, c, d, 3.0) - (y[-1] + (3.0 - x[-1]) * b[-1])) < 1e-15
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_DATA), reason='reference data not present')
+def test_predictive_transform_known_answer():
+    """construct_predictive_model (opensim_utils.py:204-222) restated on the
+    parsed model must reproduce the contact/limit parameters the reference
+    shipped already-transformed in 02905_PRE/scale/model_predictive.osim."""
+    from bioimitation.osim import load_osim
+    from bioimitation import transforms
+    shipped = load_osim(os.path.join(REF_DATA, '02905/02905_PRE/scale/model_predictive.osim'))
+    ours = transforms.construct_predictive_model(load_osim(os.path.join(REF_DATA, '02905/02905_PRE/scale/model_scaled.osim')))
+    key = lambda s: (s.name, s.body, tuple(np.round(s.loc, 9)), round(s.radius, 9))
+    assert sorted(map(key, ours.spheres)) == sorted(map(key, shipped.spheres))
+    hk = lambda h: (h.name, tuple(h.geometries), h.stiffness, h.dissipation, h.static_friction,
+                    h.dynamic_friction, h.viscous_friction, h.transition_velocity)
+    assert sorted(map(hk, ours.hc_forces)) == sorted(map(hk, shipped.hc_forces))
+    lk = lambda l: (l.name, l.coord, l.upper_stiffness, l.upper_limit, l.lower_stiffness, l.lower_limit,
+                    l.damping, l.transition)
+    assert sorted(map(lk, ours.limits)) == sorted(map(lk, shipped.limits))
+    assert abs(ours.coords['pelvis_ty'].default_value - 1.02) < 1e-15
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_DATA), reason='reference data not present')
+def test_committed_packs_are_current():
+    """The committed packs equal a fresh compile from the reference data."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), 'bioimitation-gym_amd', 'tools'))
+    import build_packs
+    from bioimitation import modelpack, refmotion, registry
+    for env_id, rec in registry.RECIPES.items():
+        model = build_packs.load_model(REF_DATA, rec)
+        ref = refmotion.load_reference_tables(os.path.join(build_packs.DATA, rec['reference']), model.coord_order)
+        fresh = modelpack.pack_bytes(modelpack.compile_pack(model, registry.env_spec(env_id), ref))
+        committed = modelpack.pack_bytes(load_pack(env_id))
+        assert fresh == committed, env_id

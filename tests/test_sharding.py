@@ -1,0 +1,79 @@
+"""Env-index sharding across ranks (world_size 2, gloo on CPU): each rank
+steps its contiguous block with the fp64 oracle; the gathered result equals a
+single-process run over all envs bit for bit, and the bench's max-over-ranks
+timing reduction works over gloo."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from bioimitation.parallel import shard_range
+
+
+def test_shard_ranges_cover_exactly():
+    for total in (1, 7, 4096, 32768):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(total, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def _rollout(lo, hi, steps=6):
+    import oracle
+    from bioimitation.registry import load_pack
+    pk = load_pack('MuscleWalkingImitation2D-v0')
+    o = oracle.Oracle(pk)
+    n = hi - lo
+    bufs = o.new_envs(n)
+    out = []
+    for i in range(n):
+        o.reset(bufs, i, (lo + i) * 7 % 133)          # reset row from the GLOBAL index
+    for t in range(steps):
+        acts = np.stack([np.random.default_rng(1000 * t + lo + i).uniform(0, 1, pk.nact) for i in range(n)])
+        obs, rew, done, info = o.batch_step(bufs, n, acts, nthreads=1)
+        out.append(np.concatenate([obs, rew[:, None], info], axis=1))
+    return np.stack(out, 1)                            # (n, steps, obs+1+info)
+
+
+def _worker(rank, world, port, total, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(os.path.dirname(here), 'bioimitation-gym_amd'),
+                    os.path.join(os.path.dirname(here), 'oracle')]
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    lo, hi = shard_range(total, rank, world)
+    mine = torch.from_numpy(_rollout(lo, hi))
+    parts = [torch.zeros((shard_range(total, r, world)[1] - shard_range(total, r, world)[0],) + tuple(mine.shape[1:]),
+                         dtype=mine.dtype) for r in range(world)]
+    dist.all_gather(parts, mine)
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        q.put((torch.cat(parts).numpy(), float(t[0])))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_sharding_is_bit_identical():
+    total = 10
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, total, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    gathered, tmax = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    single = _rollout(0, total)
+    np.testing.assert_array_equal(gathered, single)
+    assert tmax == 2.0
