@@ -125,7 +125,8 @@ def main():
         tf = os.path.join(REPO, 'profiles', 'traffic.json')
         if os.path.exists(tf):
             try:
-                traffic = json.load(open(tf)).get(f'{a.env_id}/fp{a.precision}/{n}')
+                rec = json.load(open(tf)).get(f'{a.env_id}/fp{a.precision}/{n}')
+                traffic = rec['bytes'] if rec else None    # rocprofv3 FETCH_SIZE + WRITE_SIZE per launch
             except Exception:
                 traffic = None
         line = {
