@@ -23,12 +23,18 @@ struct DCurve {
     int32_t nseg, pad;
 };
 
+/* ------------------------------------------------------------------
+ * Shared model image (SModel): the model data that lanes index at run time
+ * (lane = body, muscle, path point, sphere).  One copy per workgroup is
+ * staged into LDS at kernel start, so these lookups are ds_reads (~50 cycles)
+ * instead of lane-divergent global loads (~200+ cycles at one wave per SIMD).
+ * Curves are deduplicated (all muscles of the shipped models share one set). */
 template <typename Real>
-struct DMuscle {
+struct SMuscle {
     Real fiso, lopt, inv_lopt, lts, inv_lts, lv; /* lv = lopt * vmax */
-    Real tau_act, tau_deact, amin, beta, width, lmin, slow, mass, default_act;
+    Real tau_act, tau_deact, amin, beta, width, lmin, slow, mass, default_act, pad;
     int32_t pt_off, npt;
-    DCurve<Real> fal, fv, fpe, fse;
+    int32_t cv[4]; /* curve indices: fal, fv, fpe, fse */
 };
 
 template <typename Real>
@@ -42,40 +48,63 @@ struct DPathPt {
     Real lo, hi;
 };
 
+/* composite body: joint-local constants (lane = body in the kinematics) */
+template <typename Real>
+struct SBody {
+    Real R_pf[9], p_pf[3], R_mb[9], p_mb[3];
+    Real axis[6][3];
+    Real mass, com[3], inertia[6];
+    int32_t fn[6];          /* function per spatial-transform axis (-1 none) */
+    int32_t parent, level;  /* tree parent (-1 ground), depth               */
+};
+
+template <typename Real>
+struct SFn {
+    int32_t type, coord, off, n;
+    Real a, b;
+};
+
+template <class T> struct SDim {
+    static constexpr int NCV = T::NCURVE > 0 ? T::NCURVE : 1, NMU = T::NM > 0 ? T::NM : 1;
+    static constexpr int NPT = T::NPT > 0 ? T::NPT : 1, NFN = T::NFN > 0 ? T::NFN : 1;
+    static constexpr int NK = T::NKNOT > 0 ? T::NKNOT : 1, NCD = T::NC > 0 ? T::NC : 1, NDD = T::ND > 0 ? T::ND : 1;
+    static constexpr int NP = NDD * (NDD + 1) / 2, NSD = T::NS > 0 ? T::NS : 1, NFD = T::NF > 0 ? T::NF : 1;
+    static constexpr int NLD = T::NL > 0 ? T::NL : 1, NAD = T::NA > 0 ? T::NA : 1;
+};
+
+template <class T, typename Real>
+struct SModel {
+    using D = SDim<T>;
+    DCurve<Real> curve[D::NCV];
+    SMuscle<Real> mus[D::NMU];
+    DPathPt<Real> pt[D::NPT];
+    SBody<Real> body[T::NB];
+    SFn<Real> fn[D::NFN];
+    Real kx[D::NK], ky[D::NK], kb[D::NK], kc[D::NK], kd[D::NK];
+    /* contact spheres and Hunt-Crossley parameters (lane = sphere) */
+    Real sph_loc[D::NSD][3], sph_r[D::NSD];
+    Real cf_kk[D::NFD], cf_c[D::NFD], cf_ms[D::NFD], cf_md[D::NFD], cf_mv[D::NFD], cf_vt[D::NFD];
+    /* coordinate limit forces (lane = limit) */
+    Real lim_qup[D::NLD], lim_qlow[D::NLD], lim_kup[D::NLD], lim_klow[D::NLD], lim_damp[D::NLD], lim_trans[D::NLD];
+    /* coordinate actuators / PD gains (lane = actuator) */
+    Real ca_opt[D::NAD], ca_min[D::NAD], ca_max[D::NAD], kp[D::NAD], kv[D::NAD];
+    /* index tables */
+    int32_t coord_dof[D::NCD], dof_cb[D::NDD];
+    int32_t e_l[D::NP], e_k[D::NP], e_c[D::NP]; /* packed-lower M entry -> (row, col, subtree body) */
+    uint32_t dofmask[T::NB];
+    int32_t sph_cb[D::NSD], sph_force[D::NSD], lim_coord[D::NLD], lim_dof[D::NLD], act_dof[D::NAD];
+};
+
+/* bytes of the LDS image (16-byte granules for the cooperative copy) */
+template <class T, typename Real> constexpr size_t smodel_bytes() { return (sizeof(SModel<T, Real>) + 15) & ~size_t(15); }
+
 template <typename Real>
 struct DModel {
-    /* composite bodies */
-    Real R_pf[BIOIM_MAX_CBODY][9], p_pf[BIOIM_MAX_CBODY][3];
-    Real R_mb[BIOIM_MAX_CBODY][9], p_mb[BIOIM_MAX_CBODY][3];
-    Real axis[BIOIM_MAX_CBODY][6][3];
-    Real mass[BIOIM_MAX_CBODY], com[BIOIM_MAX_CBODY][3], inertia[BIOIM_MAX_CBODY][6];
-    int32_t fn[BIOIM_MAX_CBODY][6];
-    /* functions */
-    int32_t fn_type[BIOIM_MAX_FN], fn_coord[BIOIM_MAX_FN], fn_off[BIOIM_MAX_FN], fn_n[BIOIM_MAX_FN];
-    Real fn_a[BIOIM_MAX_FN], fn_b[BIOIM_MAX_FN];
-    Real kx[BIOIM_MAX_KNOTS], ky[BIOIM_MAX_KNOTS], kb[BIOIM_MAX_KNOTS], kc[BIOIM_MAX_KNOTS], kd[BIOIM_MAX_KNOTS];
+    /* composite bodies (wave-uniform reads: observation / reward reporting) */
+    Real mass[BIOIM_MAX_CBODY], com[BIOIM_MAX_CBODY][3];
     Real coord_default[BIOIM_MAX_COORD];
     int32_t coord_dof[BIOIM_MAX_COORD];
     Real os_R[BIOIM_MAX_OSBODY][9], os_p[BIOIM_MAX_OSBODY][3];
-    /* muscles */
-    DMuscle<Real> mus[BIOIM_MAX_MUSCLE];
-    DPathPt<Real> pt[BIOIM_MAX_PATHPT];
-    /* contact / limits / actuators */
-    Real sph_loc[BIOIM_MAX_SPHERE][3], sph_r[BIOIM_MAX_SPHERE];
-    Real cf_kk[BIOIM_MAX_CFORCE], cf_c[BIOIM_MAX_CFORCE], cf_ms[BIOIM_MAX_CFORCE], cf_md[BIOIM_MAX_CFORCE],
-        cf_mv[BIOIM_MAX_CFORCE], cf_vt[BIOIM_MAX_CFORCE];
-    Real lim_qup[BIOIM_MAX_LIMIT], lim_qlow[BIOIM_MAX_LIMIT], lim_kup[BIOIM_MAX_LIMIT], lim_klow[BIOIM_MAX_LIMIT],
-        lim_damp[BIOIM_MAX_LIMIT], lim_trans[BIOIM_MAX_LIMIT];
-    Real ca_opt[BIOIM_MAX_ACT], ca_min[BIOIM_MAX_ACT], ca_max[BIOIM_MAX_ACT];
-    Real kp[BIOIM_MAX_ACT], kv[BIOIM_MAX_ACT];
-    /* lane-parallel index tables (runtime copies of the topology) */
-    uint32_t anc[BIOIM_MAX_CBODY], dofmask[BIOIM_MAX_CBODY];
-    int32_t dof_cb[BIOIM_MAX_COORD];
-    int32_t e_l[BIOIM_MAX_COORD * (BIOIM_MAX_COORD + 1) / 2], e_k[BIOIM_MAX_COORD * (BIOIM_MAX_COORD + 1) / 2],
-        e_c[BIOIM_MAX_COORD * (BIOIM_MAX_COORD + 1) / 2];
-    int32_t sph_cb[BIOIM_MAX_SPHERE], sph_force[BIOIM_MAX_SPHERE];
-    int32_t lim_coord[BIOIM_MAX_LIMIT], lim_dof[BIOIM_MAX_LIMIT];
-    int32_t act_dof[BIOIM_MAX_ACT];
     int32_t float_origin, pad1;
     /* env semantics */
     Real w_imitate, w_effort, w_action, action_r_scale, max_actuation, total_mass, weight, moment;

@@ -35,6 +35,7 @@
 #include "topologies.h"
 
 #define DEV __device__ __forceinline__
+#define BIOIM_WG 256 /* threads per workgroup: 256 / G envs share one LDS model image */
 
 template <int I, int N, class F>
 DEV void sfor(F &&f) {
@@ -102,46 +103,35 @@ template <int G> DEV bool group_any(bool p) {
 }
 
 /* ------------------------------------------------------------ functions */
-template <typename Real>
-DEV void spline_eval(const DModel<Real> &M, int off, int n, Real q, Real &f, Real &f1, Real &f2) {
-    Real x0 = M.kx[off], xn = M.kx[off + n - 1];
-    if (q < x0) { f = M.ky[off] + (q - x0) * M.kb[off]; f1 = M.kb[off]; f2 = 0; return; }
+template <class T, typename Real>
+DEV void spline_eval(const SModel<T, Real> &SM, int off, int n, Real q, Real &f, Real &f1, Real &f2) {
+    Real x0 = SM.kx[off], xn = SM.kx[off + n - 1];
+    if (q < x0) { f = SM.ky[off] + (q - x0) * SM.kb[off]; f1 = SM.kb[off]; f2 = 0; return; }
     if (q > xn) {
         int j = off + n - 1;
-        f = M.ky[j] + (q - xn) * M.kb[j]; f1 = M.kb[j]; f2 = 0; return;
+        f = SM.ky[j] + (q - xn) * SM.kb[j]; f1 = SM.kb[j]; f2 = 0; return;
     }
     int k = 0;
-    for (int i = 1; i < n - 1; ++i) k += (q > M.kx[off + i]) ? 1 : 0;
+    for (int i = 1; i < n - 1; ++i) k += (q > SM.kx[off + i]) ? 1 : 0;
     int j = off + k;
-    Real dx = q - M.kx[j], b = M.kb[j], c = M.kc[j], d = M.kd[j];
-    f = M.ky[j] + dx * (b + dx * (c + dx * d));
+    Real dx = q - SM.kx[j], b = SM.kb[j], c = SM.kc[j], d = SM.kd[j];
+    f = SM.ky[j] + dx * (b + dx * (c + dx * d));
     f1 = b + dx * (Real(2) * c + Real(3) * dx * d);
     f2 = Real(2) * c + Real(6) * dx * d;
 }
 
-/* runtime-kind evaluation (moving path points) */
-template <typename Real>
-DEV void fn_eval_rt(const DModel<Real> &M, int fi, Real q, Real &f, Real &f1, Real &f2) {
-    int type = M.fn_type[fi];
-    if (type == BIOIM_FN_CONST) { f = M.fn_b[fi]; f1 = 0; f2 = 0; }
-    else if (type == BIOIM_FN_LINEAR) { f = M.fn_a[fi] * q + M.fn_b[fi]; f1 = M.fn_a[fi]; f2 = 0; }
+/* value and first two derivatives of function fi (fi < 0: absent axis, 0) */
+template <class T, typename Real>
+DEV void fn_eval(const SModel<T, Real> &SM, int fi, Real q, Real &f, Real &f1, Real &f2) {
+    f = 0; f1 = 0; f2 = 0;
+    if (fi < 0) return;
+    const SFn<Real> &F = SM.fn[fi];
+    if (F.type == BIOIM_FN_CONST) { f = F.b; }
+    else if (F.type == BIOIM_FN_LINEAR) { f = F.a * q + F.b; f1 = F.a; }
     else {
         Real s, s1, s2;
-        spline_eval(M, M.fn_off[fi], M.fn_n[fi], q, s, s1, s2);
-        Real a = M.fn_a[fi];
-        f = a * s; f1 = a * s1; f2 = a * s2;
-    }
-}
-
-template <int KIND, typename Real>
-DEV void fn_eval_ct(const DModel<Real> &M, int fi, Real q, Real &f, Real &f1, Real &f2) {
-    if constexpr (KIND == BIOIM_FN_CONST) { f = M.fn_b[fi]; f1 = 0; f2 = 0; }
-    else if constexpr (KIND == BIOIM_FN_LINEAR) { f = M.fn_a[fi] * q + M.fn_b[fi]; f1 = M.fn_a[fi]; f2 = 0; }
-    else {
-        Real s, s1, s2;
-        spline_eval(M, M.fn_off[fi], M.fn_n[fi], q, s, s1, s2);
-        Real a = M.fn_a[fi];
-        f = a * s; f1 = a * s1; f2 = a * s2;
+        spline_eval<T, Real>(SM, F.off, F.n, q, s, s1, s2);
+        f = F.a * s; f1 = F.a * s1; f2 = F.a * s2;
     }
 }
 
@@ -233,31 +223,59 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
 }
 
 /* ---------------------------------------------------------- LDS layout
- * One region per env (4 envs per 64-lane workgroup).  Phase 1 (streamed
- * kinematics, redundant in every lane) publishes the composite frames, the
- * Plucker columns, per-body inertias and Newton-Euler wrenches; the
- * lane-parallel phases read them and publish per-lane force slots that are
- * reduced in a fixed order (bitwise deterministic). */
+ * Per workgroup: the shared model image (SModel, bioim_device.h), then one
+ * region per env.  Phase 1 (lane-parallel kinematics) publishes frames,
+ * Plucker columns, per-body inertias and Newton-Euler wrenches; the force
+ * phases read them and publish per-lane slots that are reduced in a fixed
+ * order (bitwise deterministic).  The union region U is reused by phase 1
+ * (joint-local data), phases 2-3 (force slots) and the observation staging. */
 template <class T, typename Real> struct Lay {
     static constexpr int NB = T::NB, ND = T::ND > 0 ? T::ND : 1, NC = T::NC, NP = ND * (ND + 1) / 2;
     static constexpr int NMS = T::NM > T::NA ? T::NM : T::NA;
     static constexpr int NS = T::NS > 0 ? T::NS : 1, NL = T::NL > 0 ? T::NL : 1;
-    static constexpr int KB = 0;                 /* [NB][18]: R9 o3 w3 vO3      */
-    static constexpr int S = KB + 18 * NB;       /* [ND][6]: Omega, Vo          */
-    static constexpr int QF = S + 6 * ND;        /* [NC] coordinate values       */
-    static constexpr int IC = QF + NC;           /* [NB][10]: m, h3, J6          */
-    static constexpr int WB = IC + 10 * NB;      /* [NB][6]: n3, f3              */
-    static constexpr int ICS = WB + 6 * NB;      /* subtree sums of IC           */
-    static constexpr int WBS = ICS + 10 * NB;    /* subtree sums of WB           */
-    static constexpr int MP = WBS + 6 * NB;      /* [NP] packed lower M (+implicit) */
-    static constexpr int RHS = MP + NP;          /* [ND]                         */
-    static constexpr int TAU = RHS + ND;         /* [NMS][ND] muscle/actuator slots */
-    static constexpr int CT = TAU + NMS * ND;    /* [NS][ND] contact tau slots   */
-    static constexpr int CM = CT + NS * ND;      /* [NS][NP] contact implicit slots */
-    static constexpr int CW = CM + NS * NP;      /* [NS][8]: F3, Mo3, active     */
-    static constexpr int LIM = CW + 8 * NS;      /* [NL][4]: f, diag add, tau add */
-    static constexpr int OBS = ((LIM + 4 * NL + 1) / 2) * 2;
-    static constexpr int SIZE = ((OBS + BIOIM_OBS_MAX + 1) / 2) * 2;
+    static constexpr int CJN = 3 * ND + 8;       /* per sphere: jc[ND][3], Ft3, C3 (xx xz yy zz), pad */
+    static constexpr int KB = 0;                 /* [NB][18]: R9 o3 w3 vO3 (ground, shifted origin) */
+    static constexpr int AL = KB + 18 * NB;      /* [NB][6]: alpha3, aO3 (velocity-product accels)  */
+    static constexpr int S = AL + 6 * NB;        /* [ND][6]: Plucker columns (Omega, V at origin)   */
+    static constexpr int QF = S + 6 * ND;        /* [NC] coordinate values                          */
+    static constexpr int UF = QF + NC;           /* [NC] coordinate speeds                          */
+    static constexpr int IC = UF + NC;           /* [NB][10]: m, h3, J6                             */
+    static constexpr int WB = IC + 10 * NB;      /* [NB][6]: n3, f3                                 */
+    static constexpr int ICS = WB + 6 * NB;      /* subtree sums of IC                              */
+    static constexpr int WBS = ICS + 10 * NB;    /* subtree sums of WB                              */
+    static constexpr int MP = WBS + 6 * NB;      /* [NP] packed lower M (+implicit)                 */
+    static constexpr int RHS = MP + NP;          /* [ND]                                            */
+    static constexpr int CW = RHS + ND;          /* [NS][8]: F3, Mo3, active                        */
+    static constexpr int LIM = CW + 8 * NS;      /* [NL][4]: f, diag add, tau add                   */
+    static constexpr int U = ((LIM + 4 * NL + 1) / 2) * 2;
+    static constexpr int LOC = U;                /* phase 1: [NB][24] joint-local transform/motion  */
+    static constexpr int SL = LOC + 24 * NB;     /* phase 1: [ND][6] joint-local Plucker columns    */
+    static constexpr int TAU = U;                /* phases 2-3: [NMS][ND] muscle/actuator slots     */
+    static constexpr int CJ = TAU + NMS * ND;    /* phases 2-3: [NS][CJN] contact slots             */
+    static constexpr int OBS = U;                /* report: observation staging                     */
+    static constexpr int U1 = 24 * NB + 6 * ND, U2 = NMS * ND + NS * CJN;
+    static constexpr int USZ = U1 > U2 ? (U1 > BIOIM_OBS_MAX ? U1 : BIOIM_OBS_MAX) : (U2 > BIOIM_OBS_MAX ? U2 : BIOIM_OBS_MAX);
+    static constexpr int SIZE = ((U + USZ + 1) / 2) * 2;
+};
+
+/* compile-time facts of a topology */
+template <class T> struct TopoInfo {
+    static constexpr unsigned axes_used() {
+        unsigned m = 0;
+        for (int c = 0; c < T::NB; ++c)
+            for (int a = 0; a < 6; ++a)
+                if (T::axis_kind[c * 6 + a] >= 0) m |= 1u << a;
+        return m;
+    }
+    static constexpr int depth() {
+        int d = 0;
+        for (int c = 0; c < T::NB; ++c) {
+            int l = 1;
+            for (int p = T::parent[c]; p >= 0; p = T::parent[p]) ++l;
+            d = l > d ? l : d;
+        }
+        return d;
+    }
 };
 
 DEV void wave_sync() {
@@ -285,10 +303,6 @@ __device__ unsigned long long g_stamps[16];
 #define STAMP_DECL
 #endif
 
-template <typename Real> struct Kin {
-    Real R[9], o[3], w[3], vO[3], al[3], aO[3];
-};
-
 template <int I> DEV constexpr int tri(int k, int l) { return k * (k + 1) / 2 + l; }
 
 /* coordinate values/speeds (locked: default / 0) */
@@ -302,220 +316,261 @@ DEV void fill_coords(const DModel<Real> &M, const Real *q, const Real *u, Real *
     });
 }
 
-/* Phase 1: streamed kinematics.  Every lane computes the whole tree in
- * registers (compile-time topology; a body's registers die after its last
- * child); lane 0 publishes per body: frame + spatial velocity, the Plucker
- * columns of its dofs, its spatial inertia at the ground origin and its
- * Newton-Euler (velocity-product + gravity) wrench.  The ground-x origin is
- * shifted by x0 (floating origin; dynamics are invariant to it). */
+/* ---------------------------------------------------------- kinematics
+ * Phase 1a (lane = composite body c): the joint-local part, which depends
+ * only on c's own coordinates — the spatial-transform axes (function
+ * values and derivatives, the body-fixed rotation sequence, translations),
+ * giving the child-in-parent transform, the joint's relative velocity and
+ * velocity-product acceleration in the parent frame, and the joint's
+ * Plucker columns about the parent origin (accumulated per dof into SL). */
 template <class T, typename Real>
-DEV void kinematics(const DModel<Real> &M, const Real *qf, const Real *uf, Real x0, Real (&S)[Lay<T, Real>::ND][6],
-                    Real *lds, bool publish) {
+DEV void kin_local(const SModel<T, Real> &SM, Real *lds, int c) {
     using LY = Lay<T, Real>;
-    Kin<Real> K[T::NB];
-    sfor<0, T::NB>([&](auto cI) {
-        constexpr int c = decltype(cI)::value;
-        constexpr int p = T::parent[c];
-        Kin<Real> &k = K[c];
-        Real RP[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, oP[3] = {-x0, 0, 0}, wP[3] = {0, 0, 0}, vOP[3] = {0, 0, 0},
-             alP[3] = {0, 0, 0}, aOP[3] = {0, 0, 0};
-        if constexpr (p >= 0) {
-#pragma unroll
-            for (int i = 0; i < 9; ++i) RP[i] = K[p].R[i];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                oP[i] = K[p].o[i]; wP[i] = K[p].w[i]; vOP[i] = K[p].vO[i];
-                alP[i] = K[p].al[i]; aOP[i] = K[p].aO[i];
-            }
-        }
-        Real RGF[9], oF[3], vF[3], aF[3], t[3], t2[3];
-        mm3(RP, M.R_pf[c], RGF);
-        mv3(RP, M.p_pf[c], t);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) oF[i] = oP[i] + t[i];
-        cross3(wP, oF, t);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) vF[i] = vOP[i] + t[i];
-        cross3(alP, oF, t);
-        cross3(wP, vF, t2);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) aF[i] = aOP[i] + t[i] + t2[i];
-
-        Real RFM[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-        Real wrel[3] = {0, 0, 0}, arel[3] = {0, 0, 0}, pFM[3] = {0, 0, 0}, pd[3] = {0, 0, 0}, pdd[3] = {0, 0, 0};
-        Real ucol[3][3], f1s[6] = {0, 0, 0, 0, 0, 0};
-        sfor<0, 3>([&](auto aI) {
-            constexpr int ax = decltype(aI)::value;
-            constexpr int kind = T::axis_kind[c * 6 + ax];
-            constexpr int cc = T::axis_coord[c * 6 + ax];
-            mv3(RFM, M.axis[c][ax], ucol[ax]);
-            if constexpr (kind >= 0) {
-                Real qc = 0, uc = 0;
-                if constexpr (cc >= 0) { qc = qf[cc]; uc = uf[cc]; }
-                Real f, f1, f2;
-                fn_eval_ct<kind>(M, M.fn[c][ax], qc, f, f1, f2);
-                f1s[ax] = f1;
-                Real thd = f1 * uc, cr[3];
-                cross3(wrel, ucol[ax], cr);
-#pragma unroll
-                for (int i = 0; i < 3; ++i) arel[i] += ucol[ax][i] * (f2 * uc * uc) + cr[i] * thd;
-#pragma unroll
-                for (int i = 0; i < 3; ++i) wrel[i] += ucol[ax][i] * thd;
-                Real Rk[9];
-                axis_rot(M.axis[c][ax], f, Rk);
-                mm3(RFM, Rk, RFM);
-            }
-        });
-        sfor<3, 6>([&](auto aI) {
-            constexpr int ax = decltype(aI)::value;
-            constexpr int kind = T::axis_kind[c * 6 + ax];
-            constexpr int cc = T::axis_coord[c * 6 + ax];
-            if constexpr (kind >= 0) {
-                Real qc = 0, uc = 0;
-                if constexpr (cc >= 0) { qc = qf[cc]; uc = uf[cc]; }
-                Real f, f1, f2;
-                fn_eval_ct<kind>(M, M.fn[c][ax], qc, f, f1, f2);
-                f1s[ax] = f1;
+    constexpr unsigned USED = TopoInfo<T>::axes_used();
+    const SBody<Real> &b = SM.body[c];
+    Real RFM[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    Real wrel[3] = {0, 0, 0}, arel[3] = {0, 0, 0}, pFM[3] = {0, 0, 0}, pd[3] = {0, 0, 0}, pdd[3] = {0, 0, 0};
+    Real col[6][3];
+    int cd[6];
+    sfor<0, 6>([&](auto aI) {
+        constexpr int ax = decltype(aI)::value;
+        cd[ax] = -1;
+        if constexpr (((USED >> ax) & 1u) != 0) {
+            const int fi = b.fn[ax];
+            const int cc = fi >= 0 ? SM.fn[fi].coord : -1;
+            Real qc = 0, uc = 0;
+            if (cc >= 0) { qc = lds[LY::QF + cc]; uc = lds[LY::UF + cc]; }
+            Real f, f1, f2;
+            fn_eval<T, Real>(SM, fi, qc, f, f1, f2);
+            cd[ax] = cc >= 0 ? SM.coord_dof[cc] : -1;
+            Real a[3] = {b.axis[ax][0], b.axis[ax][1], b.axis[ax][2]};
+            if constexpr (ax < 3) {
+                Real ucol[3], cr[3];
+                mv3(RFM, a, ucol);
+                Real thd = f1 * uc;
+                cross3(wrel, ucol, cr);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
-                    Real a = M.axis[c][ax][i];
-                    pFM[i] += a * f; pd[i] += a * f1 * uc; pdd[i] += a * f2 * uc * uc;
+                    arel[i] += ucol[i] * (f2 * uc * uc) + cr[i] * thd;
+                    wrel[i] += ucol[i] * thd;
+                    col[ax][i] = ucol[i] * f1;
+                }
+                Real Rk[9];
+                axis_rot(a, f, Rk);  /* f == 0 (absent axis): identity */
+                mm3(RFM, Rk, RFM);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    pFM[i] += a[i] * f; pd[i] += a[i] * (f1 * uc); pdd[i] += a[i] * (f2 * uc * uc);
+                    col[ax][i] = a[i] * f1;
                 }
             }
-        });
-        Real wr[3], ar[3], r[3], rd[3], rdd[3];
-        mv3(RGF, wrel, wr);
-        mv3(RGF, arel, ar);
-        mv3(RGF, pFM, r);
-        mv3(RGF, pd, rd);
-        mv3(RGF, pdd, rdd);
-        Real w[3], al[3], oM[3], vM[3], aM[3];
-        cross3(wP, wr, t);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) { w[i] = wP[i] + wr[i]; al[i] = alP[i] + t[i] + ar[i]; oM[i] = oF[i] + r[i]; }
-        cross3(wP, r, t);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) vM[i] = vF[i] + t[i] + rd[i];
-        {
-            Real a1[3], a2[3], a3[3], wr2[3];
-            cross3(alP, r, a1);
-            cross3(wP, r, wr2);
-            cross3(wP, wr2, a2);
-            cross3(wP, rd, a3);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) aM[i] = aF[i] + a1[i] + a2[i] + Real(2) * a3[i] + rdd[i];
-        }
-        Real RGM[9], dd[3], oB[3], vB[3], aB[3];
-        mm3(RGF, RFM, RGM);
-        mm3(RGM, M.R_mb[c], k.R);
-        mv3(RGM, M.p_mb[c], dd);
-        cross3(w, dd, t);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) { oB[i] = oM[i] + dd[i]; vB[i] = vM[i] + t[i]; }
-        {
-            Real a1[3], a2[3], wd[3];
-            cross3(al, dd, a1);
-            cross3(w, dd, wd);
-            cross3(w, wd, a2);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) aB[i] = aM[i] + a1[i] + a2[i];
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) { k.o[i] = oB[i]; k.w[i] = w[i]; k.al[i] = al[i]; }
-        cross3(w, oB, t);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) k.vO[i] = vB[i] - t[i];
-        {
-            Real a1[3], a2[3];
-            cross3(al, oB, a1);
-            cross3(w, vB, a2);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) k.aO[i] = aB[i] - a1[i] - a2[i];
-        }
-        sfor<0, T::ND>([&](auto dI) {
-            constexpr int d = decltype(dI)::value;
-            if constexpr (T::dof_cb[d] == c) {
-                constexpr int cc = T::dof_coord[d];
-                Real Om[3] = {0, 0, 0}, Vm[3] = {0, 0, 0};
-                sfor<0, 3>([&](auto aI) {
-                    constexpr int ax = decltype(aI)::value;
-                    if constexpr (T::axis_coord[c * 6 + ax] == cc && T::axis_kind[c * 6 + ax] >= 0) {
-#pragma unroll
-                        for (int i = 0; i < 3; ++i) Om[i] += ucol[ax][i] * f1s[ax];
-                    }
-                });
-                sfor<3, 6>([&](auto aI) {
-                    constexpr int ax = decltype(aI)::value;
-                    if constexpr (T::axis_coord[c * 6 + ax] == cc && T::axis_kind[c * 6 + ax] >= 0) {
-#pragma unroll
-                        for (int i = 0; i < 3; ++i) Vm[i] += M.axis[c][ax][i] * f1s[ax];
-                    }
-                });
-                Real OG[3], VG[3], tt[3];
-                mv3(RGF, Om, OG);
-                mv3(RGF, Vm, VG);
-                cross3(OG, oM, tt);
-#pragma unroll
-                for (int i = 0; i < 3; ++i) { S[d][i] = OG[i]; S[d][3 + i] = VG[i] - tt[i]; }
-                if (publish) {
-#pragma unroll
-                    for (int i = 0; i < 6; ++i) lds[LY::S + 6 * d + i] = S[d][i];
-                }
-            }
-        });
-        if (publish) {
-            Real *kb = lds + LY::KB + 18 * c;
-#pragma unroll
-            for (int i = 0; i < 9; ++i) kb[i] = k.R[i];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) { kb[9 + i] = k.o[i]; kb[12 + i] = k.w[i]; kb[15 + i] = k.vO[i]; }
-            /* spatial inertia at the ground origin and the Newton-Euler wrench */
-            Real cl[3], cG[3];
-            mv3(k.R, M.com[c], cl);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) cG[i] = k.o[i] + cl[i];
-            Real Ib[9] = {M.inertia[c][0], M.inertia[c][3], M.inertia[c][4], M.inertia[c][3], M.inertia[c][1],
-                          M.inertia[c][5], M.inertia[c][4], M.inertia[c][5], M.inertia[c][2]};
-            Real Tm[9], RT[9], IG[9];
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-                for (int j = 0; j < 3; ++j) RT[3 * i + j] = k.R[3 * j + i];
-            mm3(k.R, Ib, Tm);
-            mm3(Tm, RT, IG);
-            Real m = M.mass[c], ccd = dot3(cG, cG);
-            Real *ic = lds + LY::IC + 10 * c;
-            ic[0] = m;
-#pragma unroll
-            for (int i = 0; i < 3; ++i) ic[1 + i] = m * cG[i];
-            ic[4] = IG[0] + m * (ccd - cG[0] * cG[0]);
-            ic[5] = IG[4] + m * (ccd - cG[1] * cG[1]);
-            ic[6] = IG[8] + m * (ccd - cG[2] * cG[2]);
-            ic[7] = IG[1] - m * cG[0] * cG[1];
-            ic[8] = IG[2] - m * cG[0] * cG[2];
-            ic[9] = IG[5] - m * cG[1] * cG[2];
-            Real vc[3], ac[3];
-            cross3(k.w, cG, t);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) vc[i] = k.vO[i] + t[i];
-            cross3(k.al, cG, t);
-            cross3(k.w, vc, t2);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) ac[i] = k.aO[i] + t[i] + t2[i];
-            Real f[3], Iw[3], Ia[3], n[3];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) f[i] = m * (ac[i] - M.gravity[i]);
-            mv3(IG, k.w, Iw);
-            mv3(IG, k.al, Ia);
-            cross3(k.w, Iw, t);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) n[i] = Ia[i] + t[i];
-            cross3(cG, f, t);
-            Real *wb = lds + LY::WB + 6 * c;
-#pragma unroll
-            for (int i = 0; i < 3; ++i) { wb[i] = n[i] + t[i]; wb[3 + i] = f[i]; }
         }
     });
+    Real dF[3], T9[9], RPB[9], pm[3], pPB[3];
+    mv3(RFM, b.p_mb, dF);
+    mm3(b.R_pf, RFM, T9);
+    mm3(T9, b.R_mb, RPB);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) pm[i] = pFM[i] + dF[i];
+    mv3(b.R_pf, pm, pPB);
+    Real *lc = lds + LY::LOC + 24 * c;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) lc[i] = RPB[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) lc[9 + i] = pPB[i] + b.p_pf[i];
+    Real t1[3], t2[3], t3[3], o[3];
+    mv3(b.R_pf, wrel, o);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) lc[12 + i] = o[i];
+    cross3(wrel, dF, t1);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) t2[i] = pd[i] + t1[i];
+    mv3(b.R_pf, t2, o);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) lc[15 + i] = o[i];
+    mv3(b.R_pf, arel, o);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) lc[18 + i] = o[i];
+    cross3(arel, dF, t2);
+    cross3(wrel, t1, t3);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) t2[i] = pdd[i] + t2[i] + t3[i];
+    mv3(b.R_pf, t2, o);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) lc[21 + i] = o[i];
+    /* Plucker columns in the parent frame, linear part at the parent origin;
+     * rotations act about the M origin pM = p_pf + R_pf pFM */
+    Real pM[3];
+    mv3(b.R_pf, pFM, pM);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) pM[i] += b.p_pf[i];
+    sfor<0, 6>([&](auto aI) {
+        constexpr int ax = decltype(aI)::value;
+        if constexpr (((USED >> ax) & 1u) != 0) {
+            if (cd[ax] >= 0) {
+                Real *sl = lds + LY::SL + 6 * cd[ax];
+                Real v[3];
+                mv3(b.R_pf, col[ax], v);
+                if constexpr (ax < 3) {
+                    Real lin[3];
+                    cross3(pM, v, lin);
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) { sl[i] += v[i]; sl[3 + i] += lin[i]; }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) sl[3 + i] += v[i];
+                }
+            }
+        }
+    });
+}
+
+/* parent frame of body c's joint (ground: identity at the shifted origin) */
+template <class T, typename Real>
+DEV void parent_frame(const Real *lds, int p, Real x0, Real *RP, Real *oP) {
+    using LY = Lay<T, Real>;
+    const bool g = p < 0;
+    const Real *kp = lds + LY::KB + 18 * (g ? 0 : p);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) RP[i] = g ? ((i % 4) == 0 ? Real(1) : Real(0)) : kp[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) oP[i] = g ? (i == 0 ? -x0 : Real(0)) : kp[9 + i];
+}
+
+/* Phase 1b (lane = body at the current tree level): compose with the parent */
+template <class T, typename Real>
+DEV void kin_compose(const SModel<T, Real> &SM, Real *lds, int c, Real x0) {
+    using LY = Lay<T, Real>;
+    const int p = SM.body[c].parent;
+    const bool g = p < 0;
+    const Real *kp = lds + LY::KB + 18 * (g ? 0 : p), *ap = lds + LY::AL + 6 * (g ? 0 : p);
+    Real RP[9], oP[3], wP[3], vOP[3], alP[3], aOP[3];
+    parent_frame<T, Real>(lds, p, x0, RP, oP);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        wP[i] = g ? Real(0) : kp[12 + i]; vOP[i] = g ? Real(0) : kp[15 + i];
+        alP[i] = g ? Real(0) : ap[i]; aOP[i] = g ? Real(0) : ap[3 + i];
+    }
+    const Real *lc = lds + LY::LOC + 24 * c;
+    Real R[9], oB[3], w[3], wrg[3], vrel[3], vO[3], al[3], t[3], t2[3], t3[3];
+    mm3(RP, lc, R);
+    mv3(RP, lc + 9, t);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) oB[i] = oP[i] + t[i];
+    mv3(RP, lc + 12, wrg);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) w[i] = wP[i] + wrg[i];
+    mv3(RP, lc + 15, vrel);
+    cross3(wrg, oB, t);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) vO[i] = vOP[i] + vrel[i] - t[i];
+    mv3(RP, lc + 18, t);
+    cross3(wP, wrg, t2);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) al[i] = alP[i] + t2[i] + t[i];
+    /* acceleration of the B origin (zero q''): parent point acceleration
+     * + Coriolis 2 wP x vrel + relative acceleration */
+    Real vpt[3], aB[3], aa[3];
+    cross3(wP, oB, t);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) vpt[i] = vOP[i] + t[i];
+    cross3(alP, oB, t);
+    cross3(wP, vpt, t2);
+    cross3(wP, vrel, t3);
+    mv3(RP, lc + 21, aa);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) aB[i] = aOP[i] + t[i] + t2[i] + Real(2) * t3[i] + aa[i];
+    Real vB[3], aO[3];
+    cross3(w, oB, t);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) vB[i] = vO[i] + t[i];
+    cross3(al, oB, t);
+    cross3(w, vB, t2);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) aO[i] = aB[i] - t[i] - t2[i];
+    Real *kb = lds + LY::KB + 18 * c, *ab = lds + LY::AL + 6 * c;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) kb[i] = R[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        kb[9 + i] = oB[i]; kb[12 + i] = w[i]; kb[15 + i] = vO[i];
+        ab[i] = al[i]; ab[3 + i] = aO[i];
+    }
+}
+
+/* Phase 1c (lane = dof): ground Plucker column */
+template <class T, typename Real>
+DEV void kin_column(const SModel<T, Real> &SM, Real *lds, int d, Real x0) {
+    using LY = Lay<T, Real>;
+    const int p = SM.body[SM.dof_cb[d]].parent;
+    Real RP[9], oP[3], Sa[3], Sl[3], t[3];
+    parent_frame<T, Real>(lds, p, x0, RP, oP);
+    const Real *sl = lds + LY::SL + 6 * d;
+    mv3(RP, sl, Sa);
+    mv3(RP, sl + 3, Sl);
+    cross3(Sa, oP, t);
+    Real *S = lds + LY::S + 6 * d;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { S[i] = Sa[i]; S[3 + i] = Sl[i] - t[i]; }
+}
+
+/* Phase 1c (lane = body): spatial inertia at the ground origin and the
+ * Newton-Euler (velocity-product + gravity) wrench */
+template <class T, typename Real>
+DEV void body_inertia(const SModel<T, Real> &SM, const DModel<Real> &M, Real *lds, int c) {
+    using LY = Lay<T, Real>;
+    const SBody<Real> &b = SM.body[c];
+    const Real *kb = lds + LY::KB + 18 * c, *ab = lds + LY::AL + 6 * c;
+    Real R[9], o[3], w[3], vO[3], al[3], aO[3];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) R[i] = kb[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { o[i] = kb[9 + i]; w[i] = kb[12 + i]; vO[i] = kb[15 + i]; al[i] = ab[i]; aO[i] = ab[3 + i]; }
+    Real cl[3], cG[3];
+    mv3(R, b.com, cl);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) cG[i] = o[i] + cl[i];
+    Real Ib[9] = {b.inertia[0], b.inertia[3], b.inertia[4], b.inertia[3], b.inertia[1],
+                  b.inertia[5], b.inertia[4], b.inertia[5], b.inertia[2]};
+    Real Tm[9], RT[9], IG[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) RT[3 * i + j] = R[3 * j + i];
+    mm3(R, Ib, Tm);
+    mm3(Tm, RT, IG);
+    Real m = b.mass, ccd = dot3(cG, cG);
+    Real *ic = lds + LY::IC + 10 * c;
+    ic[0] = m;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) ic[1 + i] = m * cG[i];
+    ic[4] = IG[0] + m * (ccd - cG[0] * cG[0]);
+    ic[5] = IG[4] + m * (ccd - cG[1] * cG[1]);
+    ic[6] = IG[8] + m * (ccd - cG[2] * cG[2]);
+    ic[7] = IG[1] - m * cG[0] * cG[1];
+    ic[8] = IG[2] - m * cG[0] * cG[2];
+    ic[9] = IG[5] - m * cG[1] * cG[2];
+    Real vc[3], ac[3], t[3], t2[3];
+    cross3(w, cG, t);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) vc[i] = vO[i] + t[i];
+    cross3(al, cG, t);
+    cross3(w, vc, t2);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) ac[i] = aO[i] + t[i] + t2[i];
+    Real f[3], Iw[3], Ia[3], n[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) f[i] = m * (ac[i] - M.gravity[i]);
+    mv3(IG, w, Iw);
+    mv3(IG, al, Ia);
+    cross3(w, Iw, t);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) n[i] = Ia[i] + t[i];
+    cross3(cG, f, t);
+    Real *wb = lds + LY::WB + 6 * c;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { wb[i] = n[i] + t[i]; wb[3 + i] = f[i]; }
 }
 
 /* symmetric 3x3 (xx yy zz xy xz yz) times v */
@@ -576,23 +631,26 @@ template <typename Real> DEV Real smooth_step_d(Real y0, Real y1, Real x0, Real 
     return (y1 - y0) * Real(30) * t * t * (Real(1) - t) * (Real(1) - t) / w;
 }
 
-/* Hunt-Crossley sphere s (this lane) vs the ground plane: publishes the
- * generalized force, (h > 0) the implicit matrix contribution, and the
- * sphere's wrench about the (shifted) ground origin. */
+/* Hunt-Crossley sphere s (this lane) vs the ground plane.  Publishes the
+ * sphere's wrench about the (shifted) ground origin (CW), and for the
+ * generalized force / implicit matrix: the contact-point Jacobian jc[ND][3],
+ * the force Ft (normal component at the implicitly advanced position) and
+ * the 3x3 implicit damping/stiffness block (h > 0), assembled per M entry
+ * and per rhs row in phase 3. */
 template <class T, typename Real>
-DEV void contact_lane(const DModel<Real> &M, const Real (&S)[Lay<T, Real>::ND][6], Real *lds, int s, Real h) {
+DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, int s, Real h) {
     using LY = Lay<T, Real>;
     constexpr int ND = LY::ND;
-    const int cb = M.sph_cb[s], fo = M.sph_force[s];
-    const uint32_t mask = M.dofmask[cb];
+    const int cb = SM.sph_cb[s], fo = SM.sph_force[s];
+    const uint32_t mask = SM.dofmask[cb];
     const Real *kb = lds + LY::KB + 18 * cb;
     Real *cw = lds + LY::CW + 8 * s;
-    Real *ct = lds + LY::CT + ND * s;
+    Real *cj = lds + LY::CJ + LY::CJN * s;
     Real Cn[3];
-    mv3(kb, M.sph_loc[s], Cn);
+    mv3(kb, SM.sph_loc[s], Cn);
 #pragma unroll
     for (int i = 0; i < 3; ++i) Cn[i] += kb[9 + i];
-    Real rad = M.sph_r[s];
+    Real rad = SM.sph_r[s];
     Real depth = rad - Cn[1];
     Real fn = 0, fH = 0, vn = 0, P[3] = {0, 0, 0}, vs[3] = {0, 0, 0};
     if (depth > 0) {
@@ -602,9 +660,9 @@ DEV void contact_lane(const DModel<Real> &M, const Real (&S)[Lay<T, Real>::ND][6
 #pragma unroll
         for (int i = 0; i < 3; ++i) vs[i] = kb[15 + i] + t[i];
         vn = -vs[1];
-        Real kk = M.cf_kk[fo];
+        Real kk = SM.cf_kk[fo];
         fH = Real(4.0 / 3.0) * kk * depth * sqrt(rad * kk * depth);
-        fn = fH * (Real(1) + Real(1.5) * M.cf_c[fo] * vn);
+        fn = fH * (Real(1) + Real(1.5) * SM.cf_c[fo] * vn);
     }
     bool active = fn > 0;
     cw[6] = active ? Real(1) : Real(0);
@@ -616,7 +674,7 @@ DEV void contact_lane(const DModel<Real> &M, const Real (&S)[Lay<T, Real>::ND][6
     Real F[3] = {0, fn, 0};
     Real vt0 = -vs[0], vt2 = -vs[2];
     Real vslip = sqrt(vt0 * vt0 + vt2 * vt2);
-    Real vtr = M.cf_vt[fo], ms = M.cf_ms[fo], md = M.cf_md[fo], mv = M.cf_mv[fo];
+    Real vtr = SM.cf_vt[fo], ms = SM.cf_ms[fo], md = SM.cf_md[fo], mv = SM.cf_mv[fo];
     Real r_ = vslip / vtr, den = Real(1) + r_ * r_;
     if (vslip != 0) {
         Real ff = fn * (fmin(r_, Real(1)) * (md + Real(2) * (ms - md) / den) + mv * vslip);
@@ -627,20 +685,20 @@ DEV void contact_lane(const DModel<Real> &M, const Real (&S)[Lay<T, Real>::ND][6
     cross3(P, F, mo);
 #pragma unroll
     for (int i = 0; i < 3; ++i) { cw[i] = F[i]; cw[3 + i] = mo[i]; }
-    Real kn = Real(1.5) * fH / depth * (Real(1) + Real(1.5) * M.cf_c[fo] * vn);
+    Real kn = Real(1.5) * fH / depth * (Real(1) + Real(1.5) * SM.cf_c[fo] * vn);
     /* implicit extra force -h*Kn*v_y (Hertz force at the advanced position) */
-    Real Fy = F[1] - (h > 0 ? h * kn * vs[1] : Real(0));
-    Real Ft[3] = {F[0], Fy, F[2]}, mt[3];
-    cross3(P, Ft, mt);
-    Real jc[ND][3];
-    sfor<0, T::ND>([&](auto dI) {
-        constexpr int d = decltype(dI)::value;
-        Real on = (mask >> d) & 1u ? Real(1) : Real(0);
-        cross3(S[d], P, jc[d]);
+    cj[3 * ND] = F[0];
+    cj[3 * ND + 1] = F[1] - (h > 0 ? h * kn * vs[1] : Real(0));
+    cj[3 * ND + 2] = F[2];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) jc[d][i] = on * (jc[d][i] + S[d][3 + i]);
-        ct[d] = on * (dot3(S[d], mt) + dot3(S[d] + 3, Ft));
-    });
+    for (int d = 0; d < ND; ++d) {
+        const Real *S = lds + LY::S + 6 * d;
+        Real on = (mask >> d) & 1u ? Real(1) : Real(0), j[3];
+        cross3(S, P, j);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) cj[3 * d + i] = on * (j[i] + S[3 + i]);
+    }
+    Real cxx = 0, cxz = 0, cyy = 0, czz = 0;
     if (h > 0) {
         Real g_s, gp;
         if (r_ < 1) {
@@ -654,19 +712,12 @@ DEV void contact_lane(const DModel<Real> &M, const Real (&S)[Lay<T, Real>::ND][6
         Real tx = 0, tz = 0;
         if (vslip > 0) { tx = vt0 / vslip; tz = vt2 / vslip; }
         Real ctt = h * fn * g_s, cq = h * fn * (gp - g_s);
-        Real cnn = h * Real(1.5) * M.cf_c[fo] * fH + h * h * kn;
-        Real C3[9] = {ctt + cq * tx * tx, 0, cq * tx * tz, 0, cnn, 0, cq * tx * tz, 0, ctt + cq * tz * tz};
-        Real *cm = lds + LY::CM + LY::NP * s;
-        sfor<0, T::ND>([&](auto lI) {
-            constexpr int l = decltype(lI)::value;
-            Real cj[3];
-            mv3(C3, jc[l], cj);
-            sfor<0, l + 1>([&](auto kI) {
-                constexpr int k2 = decltype(kI)::value;
-                cm[tri<0>(l, k2)] = dot3(jc[k2], cj);
-            });
-        });
+        cyy = h * Real(1.5) * SM.cf_c[fo] * fH + h * h * kn;
+        cxx = ctt + cq * tx * tx;
+        cxz = cq * tx * tz;
+        czz = ctt + cq * tz * tz;
     }
+    cj[3 * ND + 3] = cxx; cj[3 * ND + 4] = cxz; cj[3 * ND + 5] = cyy; cj[3 * ND + 6] = czz;
 }
 
 /* ------------------------------------------------------------ muscles */
@@ -675,9 +726,11 @@ template <typename Real> struct MState {
     bool clamped;
 };
 
-template <typename Real>
-DEV void muscle_eval(const DMuscle<Real> &mu, Real a_state, Real l_state, Real excitation, Real L, Real v_warm,
-                     MState<Real> &s) {
+template <class T, typename Real>
+DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_state, Real l_state, Real excitation,
+                     Real L, Real v_warm, MState<Real> &s) {
+    const DCurve<Real> &Cfal = SM.curve[mu.cv[0]], &Cfv = SM.curve[mu.cv[1]], &Cfpe = SM.curve[mu.cv[2]],
+                       &Cfse = SM.curve[mu.cv[3]];
     Real a = a_state < mu.amin ? mu.amin : (a_state > Real(1) ? Real(1) : a_state);
     Real lce = l_state < mu.lmin ? mu.lmin : l_state;
     Real w = mu.width;
@@ -685,18 +738,18 @@ DEV void muscle_eval(const DMuscle<Real> &mu, Real a_state, Real l_state, Real e
     Real cosphi = sq / lce;
     Real lt = L - sq;
     Real fse, dfse, fal, dfal, fpe, dfpe;
-    curve_eval(mu.fse, lt * mu.inv_lts, fse, dfse);
-    curve_eval(mu.fal, lce * mu.inv_lopt, fal, dfal);
-    curve_eval(mu.fpe, lce * mu.inv_lopt, fpe, dfpe);
+    curve_eval(Cfse, lt * mu.inv_lts, fse, dfse);
+    curve_eval(Cfal, lce * mu.inv_lopt, fal, dfal);
+    curve_eval(Cfpe, lce * mu.inv_lopt, fpe, dfpe);
     Real rhs = fse / cosphi - fpe;
     Real vN, fvv, dfv;
-    solve_fv(mu.fv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
+    solve_fv(Cfv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
     Real dGdv = a * fal * dfv + mu.beta;
     bool clamped = (l_state <= mu.lmin && vN <= 0) || l_state < mu.lmin;
     if (clamped) {
         vN = 0;
         Real y, dy;
-        curve_eval(mu.fv, Real(0), y, dy);
+        curve_eval(Cfv, Real(0), y, dy);
         fvv = y;
     }
     s.act = a;
@@ -715,17 +768,18 @@ DEV void muscle_eval(const DMuscle<Real> &mu, Real a_state, Real l_state, Real e
 }
 
 /* static fiber equilibrium at reset (zero fiber velocity) */
-template <typename Real>
-DEV Real muscle_equilibrium(const DMuscle<Real> &mu, Real a_state, Real L) {
+template <class T, typename Real>
+DEV Real muscle_equilibrium(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_state, Real L) {
+    const DCurve<Real> &Cfal = SM.curve[mu.cv[0]], &Cfpe = SM.curve[mu.cv[2]], &Cfse = SM.curve[mu.cv[3]];
     Real a = a_state < mu.amin ? mu.amin : (a_state > Real(1) ? Real(1) : a_state);
     Real w = mu.width, lo = mu.lmin;
     Real hi = sqrt((L - mu.lts) * (L - mu.lts) + w * w);
     if (!(L - mu.lts > sqrt(lo * lo - w * w))) return lo;
     {   /* the fiber out-pulls the tendon even at its minimum length: no root */
         Real sq = sqrt(lo * lo - w * w), fal, dfal, fpe, dfpe, fse, dfse;
-        curve_eval(mu.fal, lo * mu.inv_lopt, fal, dfal);
-        curve_eval(mu.fpe, lo * mu.inv_lopt, fpe, dfpe);
-        curve_eval(mu.fse, (L - sq) * mu.inv_lts, fse, dfse);
+        curve_eval(Cfal, lo * mu.inv_lopt, fal, dfal);
+        curve_eval(Cfpe, lo * mu.inv_lopt, fpe, dfpe);
+        curve_eval(Cfse, (L - sq) * mu.inv_lts, fse, dfse);
         if ((a * fal + fpe) * (sq / lo) - fse >= 0) return lo;
     }
     Real l = sqrt((L - Real(1.01) * mu.lts) * (L - Real(1.01) * mu.lts) + w * w);
@@ -733,9 +787,9 @@ DEV Real muscle_equilibrium(const DMuscle<Real> &mu, Real a_state, Real L) {
     for (int it = 0; it < 4 * Eps<Real>::it_max; ++it) {
         Real sq = sqrt(l * l - w * w), cphi = sq / l;
         Real fal, dfal, fpe, dfpe, fse, dfse;
-        curve_eval(mu.fal, l * mu.inv_lopt, fal, dfal);
-        curve_eval(mu.fpe, l * mu.inv_lopt, fpe, dfpe);
-        curve_eval(mu.fse, (L - sq) * mu.inv_lts, fse, dfse);
+        curve_eval(Cfal, l * mu.inv_lopt, fal, dfal);
+        curve_eval(Cfpe, l * mu.inv_lopt, fpe, dfpe);
+        curve_eval(Cfse, (L - sq) * mu.inv_lts, fse, dfse);
         Real H = (a * fal + fpe) * cphi - fse;
         Real dH = (a * dfal + dfpe) * mu.inv_lopt * cphi + (a * fal + fpe) * (w * w) / (l * l * sq) + dfse * mu.inv_lts / cphi;
         if (H > 0) hi = l; else lo = l;
@@ -748,12 +802,10 @@ DEV Real muscle_equilibrium(const DMuscle<Real> &mu, Real a_state, Real L) {
     return l;
 }
 
-/* path length and dL/dq of muscle m (frames from LDS, Plucker columns in registers) */
+/* path length and dL/dq of one muscle (frames and Plucker columns from LDS) */
 template <class T, typename Real>
-DEV void muscle_path(const DModel<Real> &M, const Real (&S)[Lay<T, Real>::ND][6], const Real *lds, int m, Real &L,
-                     Real *dLdq) {
+DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const Real *lds, Real &L, Real *dLdq) {
     using LY = Lay<T, Real>;
-    const DMuscle<Real> &mu = M.mus[m];
     const Real *ldsq = lds + LY::QF;
     L = 0;
 #pragma unroll
@@ -765,14 +817,15 @@ DEV void muscle_path(const DModel<Real> &M, const Real (&S)[Lay<T, Real>::ND][6]
     auto flush = [&](const Real *g) {
         Real mo[3];
         cross3(Pp, g, mo);
-        sfor<0, T::ND>([&](auto dI) {
-            constexpr int d = decltype(dI)::value;
+#pragma unroll
+        for (int d = 0; d < T::ND; ++d) {
+            const Real *S = lds + LY::S + 6 * d;
             Real on = (maskp >> d) & 1u ? Real(1) : Real(0);
-            dLdq[d] += on * (dot3(S[d], mo) + dot3(S[d] + 3, g)) + (mdofp == d ? dot3(g, dPp) : Real(0));
-        });
+            dLdq[d] += on * (dot3(S, mo) + dot3(S + 3, g)) + (mdofp == d ? dot3(g, dPp) : Real(0));
+        }
     };
     for (int j = 0; j < mu.npt; ++j) {
-        const DPathPt<Real> &pt = M.pt[mu.pt_off + j];
+        const DPathPt<Real> &pt = SM.pt[mu.pt_off + j];
         if (pt.type == BIOIM_PT_COND) {
             Real qc = ldsq[pt.cond_coord];
             if (qc < pt.lo || qc > pt.hi) continue;
@@ -784,7 +837,7 @@ DEV void muscle_path(const DModel<Real> &M, const Real (&S)[Lay<T, Real>::ND][6]
             for (int a = 0; a < 3; ++a) {
                 if (pt.fn[a] < 0) { ll[a] = pt.loc[a]; continue; }
                 Real f, f1, f2;
-                fn_eval_rt(M, pt.fn[a], ldsq[pt.mcoord], f, f1, f2);
+                fn_eval<T, Real>(SM, pt.fn[a], ldsq[pt.mcoord], f, f1, f2);
                 ll[a] = f; dl[a] = f1;
             }
             mv3(pt.R, ll, loc);
@@ -835,23 +888,39 @@ template <class T, typename Real> struct Dyn {
  * accelerations (realize).  Leaves frames, contact wrenches and limit
  * forces published in LDS for reporting. */
 template <class T, typename Real>
-DEV void dynamics(const DModel<Real> &M, const Real *q, const Real *u, Real act, Real lce, Real control, int lane,
-                  Real *lds, Real h, bool equilibrate, Dyn<T, Real> &D) {
+DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *q, const Real *u, Real act, Real lce,
+                  Real control, int lane, Real *lds, Real h, bool equilibrate, Dyn<T, Real> &D) {
     using LY = Lay<T, Real>;
     constexpr int ND = LY::ND, NP = LY::NP, NB = T::NB, G = T::G;
     STAMP_DECL
-    Real qf[T::NC], uf[T::NC];
-    fill_coords<T, Real>(M, q, u, qf, uf);
     Real x0 = 0;
-    if constexpr (T::TX >= 0) x0 = M.float_origin ? qf[T::TX] : Real(0);
-    D.x0 = x0;
-    Real S[ND][6];
-    const bool pub = (lane == 0);
-    if (pub) {
-#pragma unroll
-        for (int c = 0; c < T::NC; ++c) lds[LY::QF + c] = qf[c];
+    if constexpr (T::TX >= 0) {
+        constexpr int d = T::coord_dof[T::TX];
+        if constexpr (d >= 0) x0 = M.float_origin ? q[d] : Real(0);
     }
-    kinematics<T, Real>(M, qf, uf, x0, S, lds, pub);
+    D.x0 = x0;
+    if (lane == 0) {
+        Real qf[T::NC], uf[T::NC];
+        fill_coords<T, Real>(M, q, u, qf, uf);
+#pragma unroll
+        for (int c = 0; c < T::NC; ++c) { lds[LY::QF + c] = qf[c]; lds[LY::UF + c] = uf[c]; }
+    }
+    if (lane < ND) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) lds[LY::SL + 6 * lane + i] = 0;
+    }
+    wave_sync();
+
+    /* ---- phase 1: lane-parallel kinematics */
+    if (lane < NB) kin_local<T, Real>(SM, lds, lane);
+    wave_sync();
+    sfor<0, TopoInfo<T>::depth()>([&](auto lI) {
+        constexpr int lvl = decltype(lI)::value;
+        if (lane < NB && SM.body[lane].level == lvl) kin_compose<T, Real>(SM, lds, lane, x0);
+        wave_sync();
+    });
+    if (lane < ND) kin_column<T, Real>(SM, lds, lane, x0);
+    if (lane < NB) body_inertia<T, Real>(SM, M, lds, lane);
     wave_sync();
     STAMP(0);
 
@@ -875,44 +944,43 @@ DEV void dynamics(const DModel<Real> &M, const Real *q, const Real *u, Real act,
     STAMP(1);
     if constexpr (T::NM > 0) {
         if (lane < T::NM) {
+            const SMuscle<Real> &mu = SM.mus[lane];
             Real L, dLdq[ND];
-            muscle_path<T, Real>(M, S, lds, lane, L, dLdq);
+            muscle_path<T, Real>(SM, mu, lds, L, dLdq);
             if (equilibrate) { /* reset: default activation, static fiber equilibrium */
-                act = M.mus[lane].default_act;
-                lce = muscle_equilibrium(M.mus[lane], act, L);
+                act = mu.default_act;
+                lce = muscle_equilibrium<T, Real>(SM, mu, act, L);
             }
             D.act = act;
             D.lce = lce;
-            muscle_eval(M.mus[lane], act, lce, control, L, D.ms.vN, D.ms);
+            muscle_eval<T, Real>(SM, mu, act, lce, control, L, D.ms.vN, D.ms);
 #pragma unroll
             for (int d = 0; d < ND; ++d) lds[LY::TAU + ND * lane + d] = -D.ms.Ft * dLdq[d];
         }
     } else {
         if (lane < T::NA) {
-            int ad = M.act_dof[lane];
-            Real f = control * M.ca_opt[lane];
+            int ad = SM.act_dof[lane];
+            Real f = control * SM.ca_opt[lane];
 #pragma unroll
             for (int d = 0; d < ND; ++d) lds[LY::TAU + ND * lane + d] = (d == ad) ? f : Real(0);
         }
     }
     STAMP(2);
-    if (lane < T::NS) contact_lane<T, Real>(M, S, lds, lane, h);
+    if (lane < T::NS) contact_lane<T, Real>(SM, lds, lane, h);
     STAMP(3);
     if (lane < T::NL) {
-        int cc = M.lim_coord[lane];
-        Real qv = lds[LY::QF + cc], qd = uf[0];
-#pragma unroll
-        for (int c = 1; c < T::NC; ++c) qd = (c == cc) ? uf[c] : qd;
-        Real qup = M.lim_qup[lane], qlo = M.lim_qlow[lane], tr = M.lim_trans[lane];
+        int cc = SM.lim_coord[lane];
+        Real qv = lds[LY::QF + cc], qd = lds[LY::UF + cc];
+        Real qup = SM.lim_qup[lane], qlo = SM.lim_qlow[lane], tr = SM.lim_trans[lane];
         Real up = smooth_step(Real(0), Real(1), qup, qup + tr, qv);
         Real lo = smooth_step(Real(1), Real(0), qlo - tr, qlo, qv);
-        Real f = -M.lim_kup[lane] * up * (qv - qup) + M.lim_klow[lane] * lo * (qlo - qv) - M.lim_damp[lane] * (up + lo) * qd;
+        Real f = -SM.lim_kup[lane] * up * (qv - qup) + SM.lim_klow[lane] * lo * (qlo - qv) - SM.lim_damp[lane] * (up + lo) * qd;
         Real diag = 0, tadd = f;
         if (h > 0) {
             Real dup = smooth_step_d(Real(0), Real(1), qup, qup + tr, qv);
             Real dlo = smooth_step_d(Real(1), Real(0), qlo - tr, qlo, qv);
-            Real kq = M.lim_kup[lane] * (up + dup * (qv - qup)) + M.lim_klow[lane] * (lo - dlo * (qlo - qv));
-            Real cq = M.lim_damp[lane] * (up + lo);
+            Real kq = SM.lim_kup[lane] * (up + dup * (qv - qup)) + SM.lim_klow[lane] * (lo - dlo * (qlo - qv));
+            Real cq = SM.lim_damp[lane] * (up + lo);
             diag = h * cq + h * h * kq;
             tadd = f - h * kq * qd;
         }
@@ -924,7 +992,7 @@ DEV void dynamics(const DModel<Real> &M, const Real *q, const Real *u, Real act,
 
     /* ---- phase 3: mass-matrix entries and right-hand side, fixed-order sums */
     for (int e = lane; e < NP; e += G) {
-        int l = M.e_l[e], k = M.e_k[e], c = M.e_c[e];
+        int l = SM.e_l[e], k = SM.e_k[e], c = SM.e_c[e];
         Real v = 0;
         if (c >= 0) {
             const Real *Sl = lds + LY::S + 6 * l, *Sk = lds + LY::S + 6 * k, *ic = lds + LY::ICS + 10 * c;
@@ -941,26 +1009,33 @@ DEV void dynamics(const DModel<Real> &M, const Real *q, const Real *u, Real act,
         if (h > 0) {
 #pragma unroll
             for (int s = 0; s < T::NS; ++s)
-                if (lds[LY::CW + 8 * s + 6] > 0) v += lds[LY::CM + NP * s + e];
+                if (lds[LY::CW + 8 * s + 6] > 0) {
+                    const Real *cj = lds + LY::CJ + LY::CJN * s, *C = cj + 3 * ND + 3;
+                    const Real *jl = cj + 3 * l, *jk = cj + 3 * k;
+                    v += jl[0] * (C[0] * jk[0] + C[1] * jk[2]) + jl[1] * (C[2] * jk[1]) + jl[2] * (C[1] * jk[0] + C[3] * jk[2]);
+                }
             if (l == k)
 #pragma unroll
                 for (int li = 0; li < T::NL; ++li)
-                    if (M.lim_dof[li] == l) v += lds[LY::LIM + 4 * li + 1];
+                    if (SM.lim_dof[li] == l) v += lds[LY::LIM + 4 * li + 1];
         }
         lds[LY::MP + e] = v;
     }
     if (lane < ND) {
-        const Real *Sd = lds + LY::S + 6 * lane, *wb = lds + LY::WBS + 6 * M.dof_cb[lane];
+        const Real *Sd = lds + LY::S + 6 * lane, *wb = lds + LY::WBS + 6 * SM.dof_cb[lane];
         Real r = -(dot3(Sd, wb) + dot3(Sd + 3, wb + 3));
 #pragma unroll
         for (int m = 0; m < LY::NMS; ++m)
             if (m < (T::NM > 0 ? T::NM : T::NA)) r += lds[LY::TAU + ND * m + lane];
 #pragma unroll
         for (int s = 0; s < T::NS; ++s)
-            if (lds[LY::CW + 8 * s + 6] > 0) r += lds[LY::CT + ND * s + lane];
+            if (lds[LY::CW + 8 * s + 6] > 0) {
+                const Real *cj = lds + LY::CJ + LY::CJN * s;
+                r += dot3(cj + 3 * lane, cj + 3 * ND);
+            }
 #pragma unroll
         for (int li = 0; li < T::NL; ++li)
-            if (M.lim_dof[li] == lane) r += lds[LY::LIM + 4 * li + 2];
+            if (SM.lim_dof[li] == lane) r += lds[LY::LIM + 4 * li + 2];
         lds[LY::RHS + lane] = r;
     }
     wave_sync();
@@ -1033,22 +1108,29 @@ DEV int draw_index(uint64_t seed, int env, int count, int hi) {
  * One 64-lane workgroup = 64/G envs.  mode 0: env step (optionally with
  * in-kernel auto-reset); mode 1: reset the listed envs. */
 template <class T, typename Real>
-__global__ __launch_bounds__(64) void env_kernel(const DModel<Real> *__restrict__ Mg, DState<Real> st, int N, int mode,
-                                                 const Real *__restrict__ actions, Real *__restrict__ obs,
-                                                 Real *__restrict__ reward, uint8_t *__restrict__ done_out,
-                                                 Real *__restrict__ info, const int32_t *__restrict__ env_ids,
-                                                 const int32_t *__restrict__ ref_index, int n_list, int auto_reset,
-                                                 uint64_t seed, int env_offset) {
+__global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))) void env_kernel(
+    const DModel<Real> *__restrict__ Mg, const SModel<T, Real> *__restrict__ Sg, DState<Real> st, int N, int mode,
+    const Real *__restrict__ actions, Real *__restrict__ obs, Real *__restrict__ reward, uint8_t *__restrict__ done_out,
+    Real *__restrict__ info, const int32_t *__restrict__ env_ids, const int32_t *__restrict__ ref_index, int n_list,
+    int auto_reset, uint64_t seed, int env_offset) {
     using LY = Lay<T, Real>;
     constexpr int G = T::G, ND = LY::ND, NA = T::NA, NM = T::NM;
-    constexpr int EPB = 64 / G;
-    extern __shared__ __align__(16) unsigned char smem_raw[];
-    Real *smem = reinterpret_cast<Real *>(smem_raw);
+    constexpr int EPB = BIOIM_WG / G;
+    constexpr size_t SMB = smodel_bytes<T, Real>();
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    /* stage the shared model image (one copy per workgroup) */
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(Sg);
+        uint4 *dst = reinterpret_cast<uint4 *>(smem_raw);
+        for (int i = threadIdx.x; i < (int)(SMB / 16); i += BIOIM_WG) dst[i] = src[i];
+    }
+    __syncthreads();
+    const SModel<T, Real> &SM = *reinterpret_cast<const SModel<T, Real> *>(smem_raw);
     const DModel<Real> &M = *Mg;
     const int lane = threadIdx.x % G;
     const int slot = threadIdx.x / G;
     int gidx = blockIdx.x * EPB + slot;
-    Real *lds = smem + slot * LY::SIZE;
+    Real *lds = reinterpret_cast<Real *>(smem_raw + SMB) + slot * LY::SIZE;
     int env;
     if (mode == 1) {
         if (gidx >= n_list) return;
@@ -1071,7 +1153,9 @@ __global__ __launch_bounds__(64) void env_kernel(const DModel<Real> *__restrict_
     if (NM > 0 && lane < NM) { act = st.act[(size_t)lane * N + env]; lce = st.lce[(size_t)lane * N + env]; }
     if (lane < NA) {
         last = st.last[(size_t)lane * N + env];
-        for (int hh = 0; hh < H; ++hh) hist[hh] = st.hist[((size_t)hh * NA + lane) * N + env];
+#pragma unroll
+        for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
+            hist[hh] = hh < H ? st.hist[((size_t)hh * NA + lane) * N + env] : Real(0);
     }
     int done = 0;
     Real rew = 0, inf[5] = {0, 0, 0, 0, 0};
@@ -1095,23 +1179,31 @@ __global__ __launch_bounds__(64) void env_kernel(const DModel<Real> *__restrict_
                     constexpr int i = decltype(iI)::value;
                     if (lane == i) { xq = qf[T::pd_coord[i]]; xu = uf[T::pd_coord[i]]; }
                 });
-                if (lane < NA) a = M.kp[lane] * (raw - xq) - M.kv[lane] * xu;
+                if (lane < NA) a = SM.kp[lane] * (raw - xq) - SM.kv[lane] * xu;
             }
         }
         if (!has_last) {
             last = a;
-            for (int hh = 0; hh < H; ++hh) hist[hh] = a;
+#pragma unroll
+            for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh) hist[hh] = a;
         }
         has_last = 1;
-        for (int hh = 0; hh + 1 < H; ++hh) hist[hh] = hist[hh + 1];
-        hist[H - 1] = a;
+        /* fixed-trip loops keep the history in registers */
+#pragma unroll
+        for (int hh = 0; hh + 1 < BIOIM_MAX_HORIZON; ++hh)
+            if (hh + 1 < H) hist[hh] = hist[hh + 1];
+#pragma unroll
+        for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
+            if (hh == H - 1) hist[hh] = a;
         Real s = 0;
-        for (int hh = 0; hh < H; ++hh) s += hist[hh];
+#pragma unroll
+        for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
+            if (hh < H) s += hist[hh];
         curr = s / Real(H);
         Real phys = (T::FLAGS & BIOIM_ENV_RAW_ACTION) ? a : curr;
         bool pnan = group_any<G>(lane < NA && isnan(phys));
-        Real lo = NM > 0 ? Real(0) : M.ca_min[lane < NA ? lane : 0];
-        Real hi = NM > 0 ? Real(1) : M.ca_max[lane < NA ? lane : 0];
+        Real lo = NM > 0 ? Real(0) : SM.ca_min[lane < NA ? lane : 0];
+        Real hi = NM > 0 ? Real(1) : SM.ca_max[lane < NA ? lane : 0];
         Real v = pnan ? Real(0) : phys;
         control = lane < NA ? (v < lo ? lo : (v > hi ? hi : v)) : Real(0);
         /* ---- integrate to step_size * istep (semi-implicit substeps) */
@@ -1152,7 +1244,7 @@ __global__ __launch_bounds__(64) void env_kernel(const DModel<Real> *__restrict_
             typedef const __attribute__((address_space(4))) DModel<Real> CModel;
             CModel *Mi = (CModel *)Mg;
             asm volatile("" : "+s"(Mi));
-            dynamics<T, Real>(*(const DModel<Real> *)Mi, q, u, act, lce, control, lane, lds, sub ? dt : Real(0),
+            dynamics<T, Real>(*(const DModel<Real> *)Mi, SM, q, u, act, lce, control, lane, lds, sub ? dt : Real(0),
                               eq && NM > 0, D);
         }
         if (sub) {
@@ -1162,7 +1254,7 @@ __global__ __launch_bounds__(64) void env_kernel(const DModel<Real> *__restrict_
                 act += dt * D.ms.dadt;
                 if (!D.ms.clamped) {
                     Real ln = lce + dt * D.ms.vce / (Real(1) - dt * D.ms.dvdl);
-                    lce = ln < M.mus[lane].lmin ? M.mus[lane].lmin : ln;
+                    lce = ln < SM.mus[lane].lmin ? SM.mus[lane].lmin : ln;
                 }
             }
             --remaining;
@@ -1294,7 +1386,7 @@ __global__ __launch_bounds__(64) void env_kernel(const DModel<Real> *__restrict_
                 a_error = exp(Real(-2) * sqrt(group_sum<G>(an)));
                 Real cot = 0;
                 if (lane < NM) {
-                    const DMuscle<Real> &mu = M.mus[lane];
+                    const SMuscle<Real> &mu = SM.mus[lane];
                     Real l = mu.slow, ex = control, aa = D.ms.act, hp = Real(0.5 * 3.14159265358979323846);
                     Real fa = Real(40) * l * sin(hp * ex) + Real(133) * (Real(1) - l) * (Real(1) - cos(hp * ex));
                     Real fm = Real(74) * l * sin(hp * aa) + Real(111) * (Real(1) - l) * (Real(1) - cos(hp * aa));
@@ -1385,7 +1477,9 @@ __global__ __launch_bounds__(64) void env_kernel(const DModel<Real> *__restrict_
     if (NM > 0 && lane < NM) { st.act[(size_t)lane * N + env] = act; st.lce[(size_t)lane * N + env] = lce; }
     if (lane < NA) {
         st.last[(size_t)lane * N + env] = last;
-        for (int hh = 0; hh < H; ++hh) st.hist[((size_t)hh * NA + lane) * N + env] = hist[hh];
+#pragma unroll
+        for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
+            if (hh < H) st.hist[((size_t)hh * NA + lane) * N + env] = hist[hh];
     }
 }
 
@@ -1435,42 +1529,72 @@ template <typename Real> void convert_curve(const bioim_curve_t &s, DCurve<Real>
     d.nseg = s.nseg;
 }
 
-template <typename Real> void convert_model(const bioim_modelpack_t &p, DModel<Real> &m, const std::vector<uint32_t> &dofmask) {
+template <typename Real> void convert_model(const bioim_modelpack_t &p, DModel<Real> &m) {
     memset(&m, 0, sizeof(m));
     for (int c = 0; c < p.ncbody; ++c) {
-        const bioim_cbody_t &b = p.cbody[c];
-        for (int i = 0; i < 9; ++i) { m.R_pf[c][i] = (Real)b.R_pf[i]; m.R_mb[c][i] = (Real)b.R_mb[i]; }
-        for (int i = 0; i < 3; ++i) { m.p_pf[c][i] = (Real)b.p_pf[i]; m.p_mb[c][i] = (Real)b.p_mb[i]; m.com[c][i] = (Real)b.com[i]; }
-        for (int a = 0; a < 6; ++a) {
-            m.fn[c][a] = b.fn[a];
-            for (int i = 0; i < 3; ++i) m.axis[c][a][i] = (Real)b.axis[a][i];
-        }
-        m.mass[c] = (Real)b.mass;
-        for (int i = 0; i < 6; ++i) m.inertia[c][i] = (Real)b.inertia[i];
-    }
-    for (int f = 0; f < p.nfn; ++f) {
-        m.fn_type[f] = p.fn[f].type; m.fn_coord[f] = p.fn[f].coord; m.fn_off[f] = p.fn[f].knot_off;
-        m.fn_n[f] = p.fn[f].nknots; m.fn_a[f] = (Real)p.fn[f].a; m.fn_b[f] = (Real)p.fn[f].b;
-    }
-    for (int k = 0; k < p.nknots; ++k) {
-        m.kx[k] = (Real)p.knot_x[k]; m.ky[k] = (Real)p.knot_y[k]; m.kb[k] = (Real)p.knot_b[k];
-        m.kc[k] = (Real)p.knot_c[k]; m.kd[k] = (Real)p.knot_d[k];
+        for (int i = 0; i < 3; ++i) m.com[c][i] = (Real)p.cbody[c].com[i];
+        m.mass[c] = (Real)p.cbody[c].mass;
     }
     for (int c = 0; c < p.ncoord; ++c) { m.coord_default[c] = (Real)p.coord[c].default_value; m.coord_dof[c] = p.coord[c].dof; }
     for (int b = 0; b < p.nosbody; ++b) {
         for (int i = 0; i < 9; ++i) m.os_R[b][i] = (Real)p.osbody[b].R[i];
         for (int i = 0; i < 3; ++i) m.os_p[b][i] = (Real)p.osbody[b].p[i];
     }
+    m.w_imitate = (Real)p.w_imitate; m.w_effort = (Real)p.w_effort; m.w_action = (Real)p.w_action;
+    m.action_r_scale = (Real)p.action_r_scale; m.max_actuation = (Real)p.max_actuation;
+    m.total_mass = (Real)p.total_mass;
+    double wgt = fabs(p.total_mass * p.gravity[1]);
+    m.weight = (Real)wgt;
+    m.moment = (Real)(wgt * p.height);
+    m.torso_y_min = (Real)p.torso_y_min; m.limit_force_max = (Real)p.limit_force_max; m.acc_max = (Real)p.acc_max;
+    for (int i = 0; i < 3; ++i) m.gravity[i] = (Real)p.gravity[i];
+    m.float_origin = 1;
+    m.horizon = p.horizon; m.cycle = p.cycle; m.n_episode = p.n_episode; m.reset_hi = p.reset_hi;
+    m.nsub = p.nsub; m.nrows = p.nrows; m.obs_dim = p.obs_dim; m.info_dim = p.info_dim; m.env_flags = p.env_flags;
+    m.step_size = p.step_size;
+    for (int r = 0; r < p.nrows; ++r) {
+        m.ref_time[r] = p.ref_time[r];
+        m.ref_istep[r] = p.ref_istep[r];
+        for (int c = 0; c < p.ncoord; ++c) { m.ref_q[r][c] = (Real)p.ref_q[r][c]; m.ref_u[r][c] = (Real)p.ref_u[r][c]; }
+        for (int b = 0; b < BIOIM_NREFBODY; ++b)
+            for (int i = 0; i < 3; ++i) m.ref_x[r][b][i] = (Real)p.ref_x[r][b][i];
+    }
+}
+
+/* distinct muscle curves in first-appearance order over (fal, fv, fpe, fse)
+ * of each muscle (tools/build_packs.py: unique_curves) */
+static std::vector<const bioim_curve_t *> unique_curves(const bioim_modelpack_t &p, std::vector<int> *index) {
+    std::vector<const bioim_curve_t *> u;
+    for (int i = 0; i < p.nmuscle; ++i) {
+        const bioim_curve_t *cs[4] = {&p.muscle[i].fal, &p.muscle[i].fv, &p.muscle[i].fpe, &p.muscle[i].fse};
+        for (const bioim_curve_t *c : cs) {
+            int k = 0;
+            while (k < (int)u.size() && memcmp(u[k], c, sizeof(bioim_curve_t)) != 0) ++k;
+            if (k == (int)u.size()) u.push_back(c);
+            if (index) index->push_back(k);
+        }
+    }
+    return u;
+}
+
+/* the LDS model image of a pack (layout: bioim_device.h, SModel) */
+template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, SModel<T, Real> &m) {
+    memset(&m, 0, sizeof(m));
+    std::vector<int> cidx;
+    std::vector<const bioim_curve_t *> cu = unique_curves(p, &cidx);
+    for (size_t k = 0; k < cu.size(); ++k) convert_curve(*cu[k], m.curve[k]);
     for (int i = 0; i < p.nmuscle; ++i) {
         const bioim_muscle_t &s = p.muscle[i];
-        DMuscle<Real> &d = m.mus[i];
+        SMuscle<Real> &d = m.mus[i];
         d.fiso = (Real)s.fiso; d.lopt = (Real)s.lopt; d.inv_lopt = (Real)(1.0 / s.lopt);
         d.lts = (Real)s.lts; d.inv_lts = (Real)(1.0 / s.lts); d.lv = (Real)(s.lopt * s.vmax);
         d.tau_act = (Real)s.tau_act; d.tau_deact = (Real)s.tau_deact; d.amin = (Real)s.amin; d.beta = (Real)s.damping;
         d.width = (Real)s.width; d.lmin = (Real)s.lmin; d.slow = (Real)s.slow_twitch; d.mass = (Real)s.mass;
         d.default_act = (Real)s.default_act; d.pt_off = s.pt_off; d.npt = s.npt;
-        convert_curve(s.fal, d.fal); convert_curve(s.fv, d.fv); convert_curve(s.fpe, d.fpe); convert_curve(s.fse, d.fse);
+        for (int k = 0; k < 4; ++k) d.cv[k] = cidx[4 * i + k];
     }
+    std::vector<uint32_t> dofmask(T::NB, 0);
+    for (int c = 0; c < T::NB; ++c) dofmask[c] = T::dofmask[c];
     for (int j = 0; j < p.npathpt; ++j) {
         const bioim_pathpt_t &s = p.pathpt[j];
         DPathPt<Real> &d = m.pt[j];
@@ -1488,9 +1612,34 @@ template <typename Real> void convert_model(const bioim_modelpack_t &p, DModel<R
         for (int i = 0; i < 9; ++i) d.R[i] = (Real)s.R[i];
         d.lo = (Real)s.range_lo; d.hi = (Real)s.range_hi;
     }
+    for (int c = 0; c < p.ncbody; ++c) {
+        const bioim_cbody_t &b = p.cbody[c];
+        SBody<Real> &d = m.body[c];
+        for (int i = 0; i < 9; ++i) { d.R_pf[i] = (Real)b.R_pf[i]; d.R_mb[i] = (Real)b.R_mb[i]; }
+        for (int i = 0; i < 3; ++i) { d.p_pf[i] = (Real)b.p_pf[i]; d.p_mb[i] = (Real)b.p_mb[i]; d.com[i] = (Real)b.com[i]; }
+        for (int a = 0; a < 6; ++a) {
+            d.fn[a] = b.fn[a];
+            for (int i = 0; i < 3; ++i) d.axis[a][i] = (Real)b.axis[a][i];
+        }
+        d.mass = (Real)b.mass;
+        for (int i = 0; i < 6; ++i) d.inertia[i] = (Real)b.inertia[i];
+        d.parent = b.parent;
+        int lvl = 0;
+        for (int q = b.parent; q >= 0; q = p.cbody[q].parent) ++lvl;
+        d.level = lvl;
+    }
+    for (int f = 0; f < p.nfn; ++f) {
+        m.fn[f].type = p.fn[f].type; m.fn[f].coord = p.fn[f].coord; m.fn[f].off = p.fn[f].knot_off;
+        m.fn[f].n = p.fn[f].nknots; m.fn[f].a = (Real)p.fn[f].a; m.fn[f].b = (Real)p.fn[f].b;
+    }
+    for (int k = 0; k < p.nknots; ++k) {
+        m.kx[k] = (Real)p.knot_x[k]; m.ky[k] = (Real)p.knot_y[k]; m.kb[k] = (Real)p.knot_b[k];
+        m.kc[k] = (Real)p.knot_c[k]; m.kd[k] = (Real)p.knot_d[k];
+    }
     for (int s = 0; s < p.nsphere; ++s) {
         for (int i = 0; i < 3; ++i) m.sph_loc[s][i] = (Real)p.sphere[s].loc[i];
         m.sph_r[s] = (Real)p.sphere[s].radius;
+        m.sph_cb[s] = p.sphere[s].cbody; m.sph_force[s] = p.sphere[s].force;
     }
     for (int f = 0; f < p.ncforce; ++f) {
         const bioim_cforce_t &c = p.cforce[f];
@@ -1502,68 +1651,44 @@ template <typename Real> void convert_model(const bioim_modelpack_t &p, DModel<R
         const bioim_limit_t &s = p.limit[l];
         m.lim_qup[l] = (Real)s.qup; m.lim_qlow[l] = (Real)s.qlow; m.lim_kup[l] = (Real)s.kup;
         m.lim_klow[l] = (Real)s.klow; m.lim_damp[l] = (Real)s.damping; m.lim_trans[l] = (Real)s.trans;
+        m.lim_coord[l] = s.coord; m.lim_dof[l] = s.dof;
     }
     for (int a = 0; a < p.ncoordact; ++a) {
         m.ca_opt[a] = (Real)p.coordact[a].optimal_force;
         m.ca_min[a] = (Real)p.coordact[a].min_control;
         m.ca_max[a] = (Real)p.coordact[a].max_control;
+        m.act_dof[a] = p.coordact[a].dof;
     }
-    for (int a = 0; a < BIOIM_MAX_ACT; ++a) { m.kp[a] = (Real)p.kp[a]; m.kv[a] = (Real)p.kv[a]; }
-    m.w_imitate = (Real)p.w_imitate; m.w_effort = (Real)p.w_effort; m.w_action = (Real)p.w_action;
-    m.action_r_scale = (Real)p.action_r_scale; m.max_actuation = (Real)p.max_actuation;
-    m.total_mass = (Real)p.total_mass;
-    double wgt = fabs(p.total_mass * p.gravity[1]);
-    m.weight = (Real)wgt;
-    m.moment = (Real)(wgt * p.height);
-    m.torso_y_min = (Real)p.torso_y_min; m.limit_force_max = (Real)p.limit_force_max; m.acc_max = (Real)p.acc_max;
-    for (int i = 0; i < 3; ++i) m.gravity[i] = (Real)p.gravity[i];
-    /* lane-parallel index tables */
-    m.float_origin = 1;
-    for (int c = 0; c < p.ncbody; ++c) {
-        uint32_t anc = 1u << c;
-        for (int q = p.cbody[c].parent; q >= 0; q = p.cbody[q].parent) anc |= 1u << q;
-        m.anc[c] = anc;
-        m.dofmask[c] = dofmask[c];
-    }
+    for (int a = 0; a < p.nact && a < SDim<T>::NAD; ++a) { m.kp[a] = (Real)p.kp[a]; m.kv[a] = (Real)p.kv[a]; }
+    for (int c = 0; c < p.ncoord; ++c) m.coord_dof[c] = p.coord[c].dof;
     for (int c = 0; c < p.ncoord; ++c)
         if (p.coord[c].dof >= 0) m.dof_cb[p.coord[c].dof] = p.coord[c].cbody;
+    for (int c = 0; c < T::NB; ++c) m.dofmask[c] = T::dofmask[c];
     for (int l = 0, e = 0; l < p.ndof; ++l)
         for (int k = 0; k <= l; ++k, ++e) {
             int cl = m.dof_cb[l], ck = m.dof_cb[k];
             m.e_l[e] = l; m.e_k[e] = k;
-            m.e_c[e] = ((m.anc[cl] >> ck) & 1u) ? cl : (((m.anc[ck] >> cl) & 1u) ? ck : -1);
+            m.e_c[e] = ((T::anc[cl] >> ck) & 1u) ? cl : (((T::anc[ck] >> cl) & 1u) ? ck : -1);
         }
-    for (int s = 0; s < p.nsphere; ++s) { m.sph_cb[s] = p.sphere[s].cbody; m.sph_force[s] = p.sphere[s].force; }
-    for (int l = 0; l < p.nlimit; ++l) { m.lim_coord[l] = p.limit[l].coord; m.lim_dof[l] = p.limit[l].dof; }
-    for (int a = 0; a < p.ncoordact; ++a) m.act_dof[a] = p.coordact[a].dof;
-    m.horizon = p.horizon; m.cycle = p.cycle; m.n_episode = p.n_episode; m.reset_hi = p.reset_hi;
-    m.nsub = p.nsub; m.nrows = p.nrows; m.obs_dim = p.obs_dim; m.info_dim = p.info_dim; m.env_flags = p.env_flags;
-    m.step_size = p.step_size;
-    for (int r = 0; r < p.nrows; ++r) {
-        m.ref_time[r] = p.ref_time[r];
-        m.ref_istep[r] = p.ref_istep[r];
-        for (int c = 0; c < p.ncoord; ++c) { m.ref_q[r][c] = (Real)p.ref_q[r][c]; m.ref_u[r][c] = (Real)p.ref_u[r][c]; }
-        for (int b = 0; b < BIOIM_NREFBODY; ++b)
-            for (int i = 0; i < 3; ++i) m.ref_x[r][b][i] = (Real)p.ref_x[r][b][i];
-    }
 }
 
 /* structural match of a pack against a compiled topology */
-template <class T> bool topology_matches(const bioim_modelpack_t &p, std::vector<uint32_t> &dofmask) {
+template <class T> bool topology_matches(const bioim_modelpack_t &p) {
     if (p.ncbody != T::NB || p.ndof != T::ND || p.ncoord != T::NC || p.nmuscle != T::NM || p.nact != T::NA ||
         p.nsphere != T::NS || p.ncforce != T::NF || p.nlimit != T::NL || p.nosbody != T::NOS ||
         p.n_obs_bpos != T::NOBP || p.n_obs_bvel != T::NOBV)
         return false;
     if (p.coord_tx != T::TX || p.coord_ty != T::TY || p.coord_tz != T::TZ) return false;
+    if (p.npathpt != T::NPT || p.nfn != T::NFN || p.nknots != T::NKNOT) return false;
+    if ((int)unique_curves(p, nullptr).size() != T::NCURVE) return false;
+    if (p.nmuscle == 0 && p.nact > SDim<T>::NAD) return false;
     if (p.torso_body != T::TORSO || p.calcn_r_body != T::CALCN_R || p.calcn_l_body != T::CALCN_L) return false;
     if ((p.env_flags & 0x9fu) != T::FLAGS) return false;
-    std::vector<uint32_t> anc(T::NB);
     for (int c = 0; c < T::NB; ++c) {
         if (p.cbody[c].parent != T::parent[c]) return false;
         uint32_t m = 1u << c;
         for (int q = p.cbody[c].parent; q >= 0; q = p.cbody[q].parent) m |= 1u << q;
         if (m != T::anc[c]) return false;
-        anc[c] = m;
         for (int a = 0; a < 6; ++a) {
             int fi = p.cbody[c].fn[a];
             int kind = fi < 0 ? -1 : p.fn[fi].type, cc = fi < 0 ? -1 : p.fn[fi].coord;
@@ -1591,16 +1716,13 @@ template <class T> bool topology_matches(const bioim_modelpack_t &p, std::vector
         if (p.obs_bvel[b] != T::obs_bvel[b]) return false;
     for (int b = 0; b < BIOIM_NREFBODY; ++b)
         if (p.rw_body[b] != T::rw_body[b]) return false;
-    dofmask.assign(BIOIM_MAX_CBODY, 0);
-    for (int c = 0; c < T::NB; ++c) {
-        dofmask[c] = T::dofmask[c];
-    }
     return true;
 }
 
 struct Ops {
     int lanes;
-    size_t lds_bytes_per_env;
+    size_t lds_bytes;   /* per workgroup: model image + BIOIM_WG / lanes env regions */
+    int (*upload)(bioim_handle_t *);
     void (*launch)(bioim_handle_t *, int mode, const void *actions, void *obs, void *reward, uint8_t *done, void *info,
                    const int32_t *env_ids, const int32_t *ref_index, int n_list);
 };
@@ -1613,6 +1735,7 @@ struct bioim_handle {
     hipStream_t stream;
     bool own_stream;
     void *model;        /* DModel<Real> on device */
+    void *smodel;       /* SModel<T, Real> on device (staged into LDS per workgroup) */
     void *state_buf;    /* one allocation for every SoA array */
     size_t state_bytes;
     void *dstate;       /* DState<Real> (host copy of pointers) */
@@ -1622,30 +1745,51 @@ struct bioim_handle {
 
 namespace {
 
+template <class T, typename Real> constexpr size_t lds_bytes() {
+    return smodel_bytes<T, Real>() + (size_t)(BIOIM_WG / T::G) * Lay<T, Real>::SIZE * sizeof(Real);
+}
+
 template <class T, typename Real>
 void launch_impl(bioim_handle_t *h, int mode, const void *actions, void *obs, void *reward, uint8_t *done, void *info,
                  const int32_t *env_ids, const int32_t *ref_index, int n_list) {
-    constexpr int EPB = 64 / T::G;
+    constexpr int EPB = BIOIM_WG / T::G;
     int count = mode == 1 ? n_list : h->n;
     int blocks = (count + EPB - 1) / EPB;
-    size_t lds = (size_t)EPB * Lay<T, Real>::SIZE * sizeof(Real);
     DState<Real> st = *reinterpret_cast<DState<Real> *>(h->dstate);
-    hipLaunchKernelGGL((env_kernel<T, Real>), dim3(blocks), dim3(64), lds, h->stream,
-                       reinterpret_cast<const DModel<Real> *>(h->model), st, h->n, mode,
+    typedef SModel<T, Real> SM_t;
+    const size_t lds = lds_bytes<T, Real>();
+    const SM_t *smodel = reinterpret_cast<const SM_t *>(h->smodel);
+    hipLaunchKernelGGL((env_kernel<T, Real>), dim3(blocks), dim3(BIOIM_WG), lds, h->stream,
+                       reinterpret_cast<const DModel<Real> *>(h->model), smodel, st, h->n, mode,
                        reinterpret_cast<const Real *>(actions), reinterpret_cast<Real *>(obs),
                        reinterpret_cast<Real *>(reward), done, reinterpret_cast<Real *>(info), env_ids, ref_index,
                        n_list, h->auto_reset, h->seed, h->env_offset);
 }
 
-template <class T> bool pick(const bioim_modelpack_t &p, int precision, Ops &ops, std::vector<uint32_t> &dofmask) {
-    if (!topology_matches<T>(p, dofmask)) return false;
+template <class T, typename Real> int upload_smodel(bioim_handle_t *h) {
+    static_assert(lds_bytes<T, Real>() <= 163840, "LDS image + env regions exceed 160 KiB");
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real>()));
+    constexpr size_t B = smodel_bytes<T, Real>();
+    std::vector<unsigned char> img(B, 0);
+    build_smodel<T, Real>(h->pack, *reinterpret_cast<SModel<T, Real> *>(img.data()));
+    HIPCHK(hipMalloc(&h->smodel, B));
+    HIPCHK(hipMemcpyAsync(h->smodel, img.data(), B, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+template <class T> bool pick(const bioim_modelpack_t &p, int precision, Ops &ops) {
+    if (!topology_matches<T>(p)) return false;
     ops.lanes = T::G;
     if (precision == 64) {
         ops.launch = &launch_impl<T, double>;
-        ops.lds_bytes_per_env = Lay<T, double>::SIZE * sizeof(double);
+        ops.upload = &upload_smodel<T, double>;
+        ops.lds_bytes = lds_bytes<T, double>();
     } else {
         ops.launch = &launch_impl<T, float>;
-        ops.lds_bytes_per_env = Lay<T, float>::SIZE * sizeof(float);
+        ops.upload = &upload_smodel<T, float>;
+        ops.lds_bytes = lds_bytes<T, float>();
     }
     return true;
 }
@@ -1681,26 +1825,12 @@ template <typename Real> int alloc_state(bioim_handle_t *h) {
     state_layout<Real>(h, (char *)h->state_buf, st);
     h->dstate = st;
     DModel<Real> *hm = new DModel<Real>();
-    std::vector<uint32_t> dm(BIOIM_MAX_CBODY, 0);
-    {
-        /* recompute dofmask from the pack (same as the topology's) */
-        for (int c = 0; c < h->pack.ncbody; ++c) {
-            uint32_t anc = 1u << c;
-            for (int q = h->pack.cbody[c].parent; q >= 0; q = h->pack.cbody[q].parent) anc |= 1u << q;
-            uint32_t m = 0;
-            for (int cc = 0; cc < h->pack.ncoord; ++cc) {
-                int d = h->pack.coord[cc].dof;
-                if (d >= 0 && ((anc >> h->pack.coord[cc].cbody) & 1u)) m |= 1u << d;
-            }
-            dm[c] = m;
-        }
-    }
-    convert_model<Real>(h->pack, *hm, dm);
+    convert_model<Real>(h->pack, *hm);
     HIPCHK(hipMalloc(&h->model, sizeof(DModel<Real>)));
     HIPCHK(hipMemcpyAsync(h->model, hm, sizeof(DModel<Real>), hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     delete hm;
-    return 0;
+    return h->ops.upload(h);
 }
 
 template <typename Real> int xfer_state(bioim_handle_t *h, double *host, const double *in) {
@@ -1765,10 +1895,9 @@ int bioim_create(const bioim_modelpack_t *pack, int n_envs, int device, int prec
     if (device < 0 || device >= ndev) return fail(BIOIM_E_DEVICE, "bioim_create: bad device index");
     HIPCHK(hipSetDevice(device));
     Ops ops{};
-    std::vector<uint32_t> dofmask;
     bool found = false;
 #define BIOIM_TRY(S, NAME) \
-    if (!found) found = pick<S>(*pack, precision, ops, dofmask);
+    if (!found) found = pick<S>(*pack, precision, ops);
     BIOIM_FOR_EACH_TOPOLOGY(BIOIM_TRY)
 #undef BIOIM_TRY
     if (!found) return fail(BIOIM_E_NOKERNEL, std::string("bioim_create: no compiled kernel for the topology of ") + pack->env_id);
@@ -1795,6 +1924,7 @@ int bioim_destroy(bioim_handle_t *h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     if (h->state_buf) hipFree(h->state_buf);
     if (h->model) hipFree(h->model);
+    if (h->smodel) hipFree(h->smodel);
     if (h->dstate) {
         if (h->precision == 64) delete reinterpret_cast<DState<double> *>(h->dstate);
         else delete reinterpret_cast<DState<float> *>(h->dstate);

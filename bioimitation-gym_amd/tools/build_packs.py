@@ -70,6 +70,20 @@ def _carr(name, vals, ctype='int'):
     return f'    static constexpr {ctype} {name}[{len(vals)}] = {{{", ".join(str(int(v)) for v in vals)}}};\n'
 
 
+def unique_curves(pk):
+    """Distinct muscle curves (byte-equal bioim_curve_t), first-appearance
+    order over (fal, fv, fpe, fse) of each muscle — the order the device
+    model image stores them in (bioim_step.hip: build_smodel)."""
+    seen = []
+    for i in range(pk.nmuscle):
+        m = pk.muscle[i]
+        for name in ('fal', 'fv', 'fpe', 'fse'):
+            b = bytes(getattr(m, name))
+            if b not in seen:
+                seen.append(b)
+    return seen
+
+
 def emit_topology(struct, pk, lanes):
     nb, nd, nc, nm = pk.ncbody, pk.ndof, pk.ncoord, pk.nmuscle
     parent = [pk.cbody[c].parent for c in range(nb)]
@@ -104,6 +118,8 @@ def emit_topology(struct, pk, lanes):
     s += f'    static constexpr int NB = {nb}, ND = {nd}, NC = {nc}, NM = {nm}, NA = {pk.nact}, NS = {pk.nsphere},' \
          f' NF = {pk.ncforce}, NL = {pk.nlimit}, NOS = {pk.nosbody}, G = {lanes};\n'
     s += f'    static constexpr int NOBP = {pk.n_obs_bpos}, NOBV = {pk.n_obs_bvel};\n'
+    s += f'    static constexpr int NPT = {pk.npathpt}, NFN = {pk.nfn}, NKNOT = {pk.nknots},' \
+         f' NCURVE = {len(unique_curves(pk))};\n'
     s += f'    static constexpr int TX = {pk.coord_tx}, TY = {pk.coord_ty}, TZ = {pk.coord_tz};\n'
     s += f'    static constexpr int TORSO = {pk.torso_body}, CALCN_R = {pk.calcn_r_body}, CALCN_L = {pk.calcn_l_body};\n'
     s += f'    static constexpr unsigned FLAGS = {pk.env_flags & 0x9f}u; /* structural env flags */\n'
