@@ -102,6 +102,10 @@ template <int G> DEV bool group_any(bool p) {
     return ((b >> base) & m) != 0ull;
 }
 
+#ifdef BIOIM_STAMPS
+__device__ unsigned long long g_stamps[16];
+#endif
+
 /* ------------------------------------------------------------ functions */
 template <class T, typename Real>
 DEV void spline_eval(const SModel<T, Real> &SM, int off, int n, Real q, Real &f, Real &f1, Real &f2) {
@@ -111,8 +115,13 @@ DEV void spline_eval(const SModel<T, Real> &SM, int off, int n, Real q, Real &f,
         int j = off + n - 1;
         f = SM.ky[j] + (q - xn) * SM.kb[j]; f1 = SM.kb[j]; f2 = 0; return;
     }
+    /* interval search: fixed trip count, all loads independent (one LDS wait) */
     int k = 0;
-    for (int i = 1; i < n - 1; ++i) k += (q > SM.kx[off + i]) ? 1 : 0;
+#pragma unroll
+    for (int i = 1; i < T::NKMAX - 1; ++i) {
+        Real xi = SM.kx[off + (i < n - 1 ? i : 0)];
+        k += (i < n - 1 && q > xi) ? 1 : 0;
+    }
     int j = off + k;
     Real dx = q - SM.kx[j], b = SM.kb[j], c = SM.kc[j], d = SM.kd[j];
     f = SM.ky[j] + dx * (b + dx * (c + dx * d));
@@ -156,7 +165,8 @@ template <typename Real>
 DEV void curve_eval(const DCurve<Real> &C, Real x, Real &y, Real &dydx) {
     Real xc = x < C.x0 ? C.x0 : (x > C.x1 ? C.x1 : x);
     int k = 0;
-    for (int s = 0; s < C.nseg - 1; ++s) k += (xc > C.x[s][5]) ? 1 : 0;
+#pragma unroll
+    for (int s = 0; s < BIOIM_MAX_CURVESEG - 1; ++s) k += (s < C.nseg - 1 && xc > C.x[s][5]) ? 1 : 0;
     Real px[6], py[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) { px[i] = C.x[k][i]; py[i] = C.y[k][i]; }
@@ -176,14 +186,15 @@ DEV void curve_eval(const DCurve<Real> &C, Real x, Real &y, Real &dydx) {
 /* root of a*fal*fv(v) + beta*v = rhs (strictly increasing in v), solved in the
  * Bezier parameter of the bracketing segment, warm-started from v0 (the
  * previous substep's root) through the segment's u(x) table; returns v, fv,
- * dfv/dv.  Four safeguarded Newton steps, then (rarely) more until
+ * dfv/dv.  At least two safeguarded Newton steps, then more until
  * converged. */
 template <typename Real>
 DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0, Real &v, Real &fv, Real &dfv) {
     Real g0 = afal * C.y0 + beta * C.x0 - rhs;
     Real g1 = afal * C.y1 + beta * C.x1 - rhs;
     int k = 0;
-    for (int s = 1; s < C.nseg; ++s) k += (afal * C.y[s][0] + beta * C.x[s][0] - rhs <= 0) ? 1 : 0;
+#pragma unroll
+    for (int s = 1; s < BIOIM_MAX_CURVESEG; ++s) k += (s < C.nseg && afal * C.y[s][0] + beta * C.x[s][0] - rhs <= 0) ? 1 : 0;
     Real px[6], py[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) { px[i] = C.x[k][i]; py[i] = C.y[k][i]; }
@@ -199,16 +210,29 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
         u = ga / (ga - gb);
     }
     u = u > Real(0) && u < Real(1) ? u : Real(0.5);
-    Real lo = 0, hi = 1;
+    Real lo = 0, hi = 1, dprev = 1;
     for (int it = 0; it < Eps<Real>::it_max; ++it) {
         Real g = afal * bez5(py, u) + beta * bez5(px, u) - rhs;
         if (g > 0) hi = u; else lo = u;
         Real dg = afal * dbez5(py, u) + beta * dbez5(px, u);
         Real un = u - g / dg;
-        if (!(un > lo && un < hi)) un = Real(0.5) * (lo + hi);
-        Real du = un - u;
+        /* inclusive bracket: a converged step (un == u == lo or hi after
+         * rounding) must not trigger the bisection fallback */
+        if (!(un >= lo && un <= hi)) un = Real(0.5) * (lo + hi);
+        Real du = fabs(un - u);
         u = un;
-        if (it >= 3 && fabs(du) <= Eps<Real>::u_tol) break;
+        /* converged, or stagnating at the rounding level of g */
+        if (it >= 1 && (du <= Eps<Real>::u_tol || (du <= Real(1e3) * Eps<Real>::u_tol && du >= Real(0.5) * dprev))) {
+#ifdef BIOIM_STAMPS
+            if (blockIdx.x == 0 && threadIdx.x < 14) atomicAdd(&g_stamps[12], (unsigned long long)(it + 1));
+            if (blockIdx.x == 0 && threadIdx.x < 14) atomicAdd(&g_stamps[13], 1ull);
+#endif
+            break;
+        }
+#ifdef BIOIM_STAMPS
+        if (it == Eps<Real>::it_max - 1 && blockIdx.x == 0 && threadIdx.x < 14) atomicAdd(&g_stamps[14], 1ull);
+#endif
+        dprev = du;
     }
     v = bez5(px, u);
     fv = bez5(py, u);
@@ -287,7 +311,6 @@ DEV void wave_sync() {
 /* Diagnostic build only (-DBIOIM_STAMPS, tools/stamps.py): per-phase shader
  * cycles of the first env of workgroup 0, accumulated over one launch. */
 #ifdef BIOIM_STAMPS
-__device__ unsigned long long g_stamps[16];
 #define STAMP(i)                                                                      \
     do {                                                                              \
         __builtin_amdgcn_sched_barrier(0);                                            \
@@ -782,7 +805,7 @@ DEV Real muscle_equilibrium(const SModel<T, Real> &SM, const SMuscle<Real> &mu, 
         curve_eval(Cfse, (L - sq) * mu.inv_lts, fse, dfse);
         if ((a * fal + fpe) * (sq / lo) - fse >= 0) return lo;
     }
-    Real l = sqrt((L - Real(1.01) * mu.lts) * (L - Real(1.01) * mu.lts) + w * w);
+    Real l = sqrt((L - Real(1.01) * mu.lts) * (L - Real(1.01) * mu.lts) + w * w), dprev = 1;
     if (!(l > lo && l < hi)) l = Real(0.5) * (lo + hi);
     for (int it = 0; it < 4 * Eps<Real>::it_max; ++it) {
         Real sq = sqrt(l * l - w * w), cphi = sq / l;
@@ -794,10 +817,11 @@ DEV Real muscle_equilibrium(const SModel<T, Real> &SM, const SMuscle<Real> &mu, 
         Real dH = (a * dfal + dfpe) * mu.inv_lopt * cphi + (a * fal + fpe) * (w * w) / (l * l * sq) + dfse * mu.inv_lts / cphi;
         if (H > 0) hi = l; else lo = l;
         Real ln = l - H / dH;
-        if (!(ln > lo && ln < hi)) ln = Real(0.5) * (lo + hi);
-        Real dl = ln - l;
+        if (!(ln >= lo && ln <= hi)) ln = Real(0.5) * (lo + hi);
+        Real dl = fabs(ln - l);
         l = ln;
-        if (fabs(dl) <= Eps<Real>::l_tol) break;
+        if (dl <= Eps<Real>::l_tol || (it >= 1 && dl <= Real(1e3) * Eps<Real>::l_tol && dl >= Real(0.5) * dprev)) break;
+        dprev = dl;
     }
     return l;
 }
@@ -914,15 +938,17 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
     /* ---- phase 1: lane-parallel kinematics */
     if (lane < NB) kin_local<T, Real>(SM, lds, lane);
     wave_sync();
+    STAMP(0);
     sfor<0, TopoInfo<T>::depth()>([&](auto lI) {
         constexpr int lvl = decltype(lI)::value;
         if (lane < NB && SM.body[lane].level == lvl) kin_compose<T, Real>(SM, lds, lane, x0);
         wave_sync();
     });
+    STAMP(1);
     if (lane < ND) kin_column<T, Real>(SM, lds, lane, x0);
     if (lane < NB) body_inertia<T, Real>(SM, M, lds, lane);
     wave_sync();
-    STAMP(0);
+    STAMP(2);
 
     /* ---- phase 2: lane-parallel force elements */
     if (lane < NB) { /* subtree sums of inertia and wrench */
@@ -941,12 +967,13 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
 #pragma unroll
         for (int i = 0; i < 6; ++i) lds[LY::WBS + 6 * lane + i] = wb[i];
     }
-    STAMP(1);
+    STAMP(3);
     if constexpr (T::NM > 0) {
         if (lane < T::NM) {
             const SMuscle<Real> &mu = SM.mus[lane];
             Real L, dLdq[ND];
             muscle_path<T, Real>(SM, mu, lds, L, dLdq);
+            STAMP(4);
             if (equilibrate) { /* reset: default activation, static fiber equilibrium */
                 act = mu.default_act;
                 lce = muscle_equilibrium<T, Real>(SM, mu, act, L);
@@ -965,9 +992,9 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
             for (int d = 0; d < ND; ++d) lds[LY::TAU + ND * lane + d] = (d == ad) ? f : Real(0);
         }
     }
-    STAMP(2);
+    STAMP(5);
     if (lane < T::NS) contact_lane<T, Real>(SM, lds, lane, h);
-    STAMP(3);
+    STAMP(6);
     if (lane < T::NL) {
         int cc = SM.lim_coord[lane];
         Real qv = lds[LY::QF + cc], qd = lds[LY::UF + cc];
@@ -988,7 +1015,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
         lm[0] = f; lm[1] = diag; lm[2] = tadd;
     }
     wave_sync();
-    STAMP(4);
+    STAMP(7);
 
     /* ---- phase 3: mass-matrix entries and right-hand side, fixed-order sums */
     for (int e = lane; e < NP; e += G) {
@@ -1007,13 +1034,15 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
             v = dot3(Sk, Lm) + dot3(Sk + 3, Pm);
         }
         if (h > 0) {
+            /* branch-free: every slot is read (independent loads), inactive
+             * spheres (stale slots) are dropped by a select */
 #pragma unroll
-            for (int s = 0; s < T::NS; ++s)
-                if (lds[LY::CW + 8 * s + 6] > 0) {
-                    const Real *cj = lds + LY::CJ + LY::CJN * s, *C = cj + 3 * ND + 3;
-                    const Real *jl = cj + 3 * l, *jk = cj + 3 * k;
-                    v += jl[0] * (C[0] * jk[0] + C[1] * jk[2]) + jl[1] * (C[2] * jk[1]) + jl[2] * (C[1] * jk[0] + C[3] * jk[2]);
-                }
+            for (int s = 0; s < T::NS; ++s) {
+                const Real *cj = lds + LY::CJ + LY::CJN * s, *C = cj + 3 * ND + 3;
+                const Real *jl = cj + 3 * l, *jk = cj + 3 * k;
+                Real term = jl[0] * (C[0] * jk[0] + C[1] * jk[2]) + jl[1] * (C[2] * jk[1]) + jl[2] * (C[1] * jk[0] + C[3] * jk[2]);
+                v += lds[LY::CW + 8 * s + 6] > 0 ? term : Real(0);
+            }
             if (l == k)
 #pragma unroll
                 for (int li = 0; li < T::NL; ++li)
@@ -1028,18 +1057,18 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
         for (int m = 0; m < LY::NMS; ++m)
             if (m < (T::NM > 0 ? T::NM : T::NA)) r += lds[LY::TAU + ND * m + lane];
 #pragma unroll
-        for (int s = 0; s < T::NS; ++s)
-            if (lds[LY::CW + 8 * s + 6] > 0) {
-                const Real *cj = lds + LY::CJ + LY::CJN * s;
-                r += dot3(cj + 3 * lane, cj + 3 * ND);
-            }
+        for (int s = 0; s < T::NS; ++s) {
+            const Real *cj = lds + LY::CJ + LY::CJN * s;
+            Real term = dot3(cj + 3 * lane, cj + 3 * ND);
+            r += lds[LY::CW + 8 * s + 6] > 0 ? term : Real(0);
+        }
 #pragma unroll
         for (int li = 0; li < T::NL; ++li)
             if (SM.lim_dof[li] == lane) r += lds[LY::LIM + 4 * li + 2];
         lds[LY::RHS + lane] = r;
     }
     wave_sync();
-    STAMP(5);
+    STAMP(8);
 
     /* ---- phase 4: redundant Cholesky solve in registers */
     Real A[NP];
@@ -1049,7 +1078,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
     for (int d = 0; d < ND; ++d) D.qdd[d] = lds[LY::RHS + d];
     D.ok = cholesky_solve<ND, Real>(A, D.qdd);
     wave_sync();
-    STAMP(6);
+    STAMP(9);
 }
 
 /* body origin position/velocity of OpenSim body OB (-1 = system COM), in
@@ -1118,6 +1147,9 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
     constexpr int EPB = BIOIM_WG / G;
     constexpr size_t SMB = smodel_bytes<T, Real>();
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+#ifdef BIOIM_STAMPS
+    const unsigned long long k_t0 = __builtin_amdgcn_s_memtime();
+#endif
     /* stage the shared model image (one copy per workgroup) */
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(Sg);
@@ -1125,6 +1157,10 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
         for (int i = threadIdx.x; i < (int)(SMB / 16); i += BIOIM_WG) dst[i] = src[i];
     }
     __syncthreads();
+#ifdef BIOIM_STAMPS
+    const unsigned long long k_t1 = __builtin_amdgcn_s_memtime();
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[11] += k_t1 - k_t0;
+#endif
     const SModel<T, Real> &SM = *reinterpret_cast<const SModel<T, Real> *>(smem_raw);
     const DModel<Real> &M = *Mg;
     const int lane = threadIdx.x % G;
@@ -1458,6 +1494,9 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
         break;
     }
 
+#ifdef BIOIM_STAMPS
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[10] += __builtin_amdgcn_s_memtime() - k_t1;
+#endif
     /* ---- store state */
     if (lane == 0) {
         st.t[env] = t;
@@ -1680,6 +1719,8 @@ template <class T> bool topology_matches(const bioim_modelpack_t &p) {
         return false;
     if (p.coord_tx != T::TX || p.coord_ty != T::TY || p.coord_tz != T::TZ) return false;
     if (p.npathpt != T::NPT || p.nfn != T::NFN || p.nknots != T::NKNOT) return false;
+    for (int f = 0; f < p.nfn; ++f)
+        if (p.fn[f].nknots > T::NKMAX) return false;
     if ((int)unique_curves(p, nullptr).size() != T::NCURVE) return false;
     if (p.nmuscle == 0 && p.nact > SDim<T>::NAD) return false;
     if (p.torso_body != T::TORSO || p.calcn_r_body != T::CALCN_R || p.calcn_l_body != T::CALCN_L) return false;

@@ -119,7 +119,8 @@ def emit_topology(struct, pk, lanes):
          f' NF = {pk.ncforce}, NL = {pk.nlimit}, NOS = {pk.nosbody}, G = {lanes};\n'
     s += f'    static constexpr int NOBP = {pk.n_obs_bpos}, NOBV = {pk.n_obs_bvel};\n'
     s += f'    static constexpr int NPT = {pk.npathpt}, NFN = {pk.nfn}, NKNOT = {pk.nknots},' \
-         f' NCURVE = {len(unique_curves(pk))};\n'
+         f' NCURVE = {len(unique_curves(pk))},' \
+         f' NKMAX = {max([pk.fn[i].nknots for i in range(pk.nfn)] + [2])};\n'
     s += f'    static constexpr int TX = {pk.coord_tx}, TY = {pk.coord_ty}, TZ = {pk.coord_tz};\n'
     s += f'    static constexpr int TORSO = {pk.torso_body}, CALCN_R = {pk.calcn_r_body}, CALCN_L = {pk.calcn_l_body};\n'
     s += f'    static constexpr unsigned FLAGS = {pk.env_flags & 0x9f}u; /* structural env flags */\n'

@@ -1,0 +1,18 @@
+"""Summarise tools/pmc_sq.sh output: per-dispatch average of each counter
+over the env-kernel step dispatches (the first, reset, dispatch skipped)."""
+import csv
+import glob
+import os
+import sys
+
+d = sys.argv[1]
+vals = {}
+for f in sorted(glob.glob(os.path.join(d, 'p*', '*counter_collection.csv'))):
+    rows = [r for r in csv.DictReader(open(f)) if 'env_kernel' in r['Kernel_Name']]
+    disp = sorted({int(r['Dispatch_Id']) for r in rows})[1:]
+    for r in rows:
+        if int(r['Dispatch_Id']) in disp:
+            vals.setdefault(r['Counter_Name'], []).append(float(r['Counter_Value']))
+for k, v in vals.items():
+    n = len(v) and len({0})
+    print(f'{k:28s} {sum(v) / max(1, len(v)):16.4g}  (n={len(v)})')

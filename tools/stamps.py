@@ -16,6 +16,7 @@ env = VectorEnv(env_id, 4096, precision=prec, seed=1, auto_reset=True)
 env.reset()
 buf = (C.c_ulonglong * 16)()
 steps = 30
+steps = 30
 acts = torch.rand((steps + 5, 4096, env.action_dim), device=env.device, dtype=env.dtype)
 for k in range(5):
     env.step(acts[k])
@@ -25,10 +26,15 @@ for k in range(steps):
     env.step(acts[5 + k])
 torch.cuda.synchronize()
 f(buf, 1)
-names = ['kinematics(redundant)+publish', 'subtree sums', 'muscles/actuators', 'contacts', 'limits+sync',
-         'M entries + rhs', 'cholesky']
-tot = sum(buf[i] for i in range(7))
+names = ['kin local (lane=body)', 'kin compose (levels)', 'columns + inertias', 'subtree sums', 'muscle path',
+         'muscle eval / actuators', 'contacts', 'limits + sync', 'M entries + rhs', 'cholesky']
+tot = sum(buf[i] for i in range(len(names)))
 calls = steps * (env.nsub + 1)
-print(f'{env_id} fp{prec}: cycles per dynamics call {tot / calls:.0f}')
+print(f'{env_id} fp{prec}: cycles per dynamics call {tot / calls:.0f} (workgroup 0, env 0)')
 for i, n in enumerate(names):
     print(f'  {n:32s} {buf[i] / calls:9.0f} cyc  {100.0 * buf[i] / tot:5.1f} %')
+print(f'  per launch: loop {buf[10] / steps:.0f} cyc, of which dynamics {tot / steps:.0f}; '
+      f'model-image staging {buf[11] / steps:.0f} cyc')
+if buf[13]:
+    print(f'  solve_fv (wg 0, env 0 lanes): mean iterations {buf[12] / buf[13]:.2f} over {buf[13]} solves, '
+          f'{buf[14]} hit it_max')
