@@ -54,14 +54,42 @@ struct SBody {
     Real R_pf[9], p_pf[3], R_mb[9], p_mb[3];
     Real axis[6][3];
     Real mass, com[3], inertia[6];
-    int32_t fn[6];          /* function per spatial-transform axis (-1 none) */
-    int32_t parent, level;  /* tree parent (-1 ground), depth               */
+    int32_t fn[6];          /* function per spatial-transform axis (-1 none)      */
+    int32_t parent, pslot;  /* tree parent (-1 ground); its frame slot (ground NB) */
 };
 
 template <typename Real>
 struct SFn {
     int32_t type, coord, off, n;
     Real a, b;
+};
+
+/* compile-time facts of a topology (topologies.h) */
+template <class T> struct TopoInfo {
+    /* spatial-transform axes used by any body */
+    static constexpr unsigned axes_used() {
+        unsigned m = 0;
+        for (int c = 0; c < T::NB; ++c)
+            for (int a = 0; a < 6; ++a)
+                if (T::axis_kind[c * 6 + a] >= 0) m |= 1u << a;
+        return m;
+    }
+    /* function kinds at axis a over all bodies: bit (kind + 1), kind -1 = absent */
+    static constexpr unsigned axis_kinds(int a) {
+        unsigned m = 0;
+        for (int c = 0; c < T::NB; ++c) m |= 1u << (T::axis_kind[c * 6 + a] + 1);
+        return m;
+    }
+    static constexpr int depth_of(int c) {
+        int l = 1;
+        for (int p = T::parent[c]; p >= 0; p = T::parent[p]) ++l;
+        return l;
+    }
+    static constexpr int depth() {
+        int d = 0;
+        for (int c = 0; c < T::NB; ++c) d = depth_of(c) > d ? depth_of(c) : d;
+        return d;
+    }
 };
 
 template <class T> struct SDim {
@@ -92,6 +120,8 @@ struct SModel {
     int32_t coord_dof[D::NCD], dof_cb[D::NDD];
     int32_t e_l[D::NP], e_k[D::NP], e_c[D::NP]; /* packed-lower M entry -> (row, col, subtree body) */
     uint32_t dofmask[T::NB];
+    /* root-to-body joint chain, front-padded with the identity joint slot NB */
+    int32_t chain[T::NB][TopoInfo<T>::depth()];
     int32_t sph_cb[D::NSD], sph_force[D::NSD], lim_coord[D::NLD], lim_dof[D::NLD], act_dof[D::NAD];
 };
 

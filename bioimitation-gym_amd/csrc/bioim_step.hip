@@ -80,10 +80,11 @@ template <typename Real> DEV void mm3(const Real *A, const Real *B, Real *C) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) C[i] = T[i];
 }
+DEV void sincos_rt(double x, double &s, double &c);
+DEV void sincos_rt(float x, float &s, float &c);
 template <typename Real> DEV void axis_rot(const Real *a, Real th, Real *R) {
     Real s, c;
-    s = sin(th);
-    c = cos(th);
+    sincos_rt(th, s, c);
     Real t = Real(1) - c, x = a[0], y = a[1], z = a[2];
     R[0] = t * x * x + c;     R[1] = t * x * y - s * z; R[2] = t * x * z + s * y;
     R[3] = t * x * y + s * z; R[4] = t * y * y + c;     R[5] = t * y * z - s * x;
@@ -143,6 +144,67 @@ DEV void fn_eval(const SModel<T, Real> &SM, int fi, Real q, Real &f, Real &f1, R
         f = F.a * s; f1 = F.a * s1; f2 = F.a * s2;
     }
 }
+
+/* fn_eval specialised to the function kinds KM (bit kind+1; bit 0 = absent
+ * axis) that can occur at this call site (compile-time, per topology axis) */
+template <unsigned KM, class T, typename Real>
+DEV void fn_eval_km(const SModel<T, Real> &SM, int fi, Real q, Real &f, Real &f1, Real &f2) {
+    constexpr bool ABS = (KM & 1u) != 0, CON = (KM & 2u) != 0, LIN = (KM & 4u) != 0, SPL = (KM & 8u) != 0;
+    f = 0; f1 = 0; f2 = 0;
+    if constexpr (!CON && !LIN && !SPL) return;
+    const SFn<Real> &F = SM.fn[ABS ? (fi < 0 ? 0 : fi) : fi];
+    const Real a = F.a, b = F.b;
+    const int type = F.type;
+    Real v = 0, v1 = 0, v2 = 0;
+    if constexpr (LIN && CON) { const bool lin = type == BIOIM_FN_LINEAR; v = lin ? a * q + b : b; v1 = lin ? a : Real(0); }
+    else if constexpr (LIN) { v = a * q + b; v1 = a; }
+    else if constexpr (CON) { v = b; }
+    if constexpr (SPL) {
+        if (type == BIOIM_FN_SPLINE) {
+            Real s0, s1, s2;
+            spline_eval<T, Real>(SM, F.off, F.n, q, s0, s1, s2);
+            v = a * s0; v1 = a * s1; v2 = a * s2;
+        }
+    }
+    const bool present = !ABS || fi >= 0;
+    f = present ? v : Real(0); f1 = present ? v1 : Real(0); f2 = present ? v2 : Real(0);
+}
+
+/* sin and cos with one shared range reduction.  fp64: Cody-Waite reduction
+ * by pi/2 (three-part constant, exact for |x| < 1e5, far beyond joint
+ * angles) and Taylor polynomials on [-pi/4, pi/4] (truncation < 1e-19);
+ * agrees with libm to ~1 ulp.  fp32: the device sincosf. */
+DEV void sincos_rt(double x, double &s, double &c) {
+    const double k = rint(x * 0.63661977236758134308);
+    double r = fma(-k, 1.57079632679489655800e+00, x);
+    r = fma(-k, 6.12323399573676603587e-17, r);
+    r = fma(-k, -1.4973849048591698e-33, r);
+    const double r2 = r * r;
+    double ps = 2.8114572543455208e-15;                /* 1/17! */
+    ps = fma(ps, r2, -7.6471637318198164e-13);         /* -1/15! */
+    ps = fma(ps, r2, 1.6059043836821613e-10);          /* 1/13! */
+    ps = fma(ps, r2, -2.5052108385441720e-08);         /* -1/11! */
+    ps = fma(ps, r2, 2.7557319223985893e-06);          /* 1/9! */
+    ps = fma(ps, r2, -1.9841269841269841e-04);         /* -1/7! */
+    ps = fma(ps, r2, 8.3333333333333333e-03);          /* 1/5! */
+    ps = fma(ps, r2, -1.6666666666666667e-01);         /* -1/3! */
+    const double sr = fma(ps * r2, r, r);
+    double pc = 1.5619206968586225e-16;                /* 1/18! */
+    pc = fma(pc, r2, -4.7794773323873853e-14);         /* -1/16! */
+    pc = fma(pc, r2, 1.1470745597729725e-11);          /* 1/14! */
+    pc = fma(pc, r2, -2.0876756987868099e-09);         /* -1/12! */
+    pc = fma(pc, r2, 2.7557319223985891e-07);          /* 1/10! */
+    pc = fma(pc, r2, -2.4801587301587302e-05);         /* -1/8! */
+    pc = fma(pc, r2, 1.3888888888888889e-03);          /* 1/6! */
+    pc = fma(pc, r2, -4.1666666666666667e-02);         /* -1/4! */
+    pc = fma(pc, r2, 0.5);
+    const double cr = fma(-pc, r2, 1.0);
+    const int q = (int)k & 3;
+    const double ss = (q & 1) ? cr : sr, cc = (q & 1) ? sr : cr;
+    s = (q & 2) ? -ss : ss;
+    c = ((q + 1) & 2) ? -cc : cc;
+}
+DEV void sincos_rt(float x, float &s, float &c) { sincosf(x, &s, &c); }
 
 /* ----------------------------------------------------- smooth curves */
 template <typename Real> DEV Real bez5(const Real *p, Real u) {
@@ -258,9 +320,9 @@ template <class T, typename Real> struct Lay {
     static constexpr int NMS = T::NM > T::NA ? T::NM : T::NA;
     static constexpr int NS = T::NS > 0 ? T::NS : 1, NL = T::NL > 0 ? T::NL : 1;
     static constexpr int CJN = 3 * ND + 8;       /* per sphere: jc[ND][3], Ft3, C3 (xx xz yy zz), pad */
-    static constexpr int KB = 0;                 /* [NB][18]: R9 o3 w3 vO3 (ground, shifted origin) */
-    static constexpr int AL = KB + 18 * NB;      /* [NB][6]: alpha3, aO3 (velocity-product accels)  */
-    static constexpr int S = AL + 6 * NB;        /* [ND][6]: Plucker columns (Omega, V at origin)   */
+    static constexpr int KB = 0;                 /* [NB+1][18]: R9 o3 w3 vO3 (slot NB: ground)      */
+    static constexpr int AL = KB + 18 * (NB + 1); /* [NB+1][6]: alpha3, aO3 (velocity-product accels) */
+    static constexpr int S = AL + 6 * (NB + 1);  /* [ND][6]: Plucker columns (Omega, V at origin)   */
     static constexpr int QF = S + 6 * ND;        /* [NC] coordinate values                          */
     static constexpr int UF = QF + NC;           /* [NC] coordinate speeds                          */
     static constexpr int IC = UF + NC;           /* [NB][10]: m, h3, J6                             */
@@ -272,34 +334,14 @@ template <class T, typename Real> struct Lay {
     static constexpr int CW = RHS + ND;          /* [NS][8]: F3, Mo3, active                        */
     static constexpr int LIM = CW + 8 * NS;      /* [NL][4]: f, diag add, tau add                   */
     static constexpr int U = ((LIM + 4 * NL + 1) / 2) * 2;
-    static constexpr int LOC = U;                /* phase 1: [NB][24] joint-local transform/motion  */
-    static constexpr int SL = LOC + 24 * NB;     /* phase 1: [ND][6] joint-local Plucker columns    */
+    static constexpr int LOC = U;                /* phase 1: [NB+1][24] joint-local data (NB: identity) */
+    static constexpr int SL = LOC + 24 * (NB + 1); /* phase 1: [ND][6] joint-local Plucker columns  */
     static constexpr int TAU = U;                /* phases 2-3: [NMS][ND] muscle/actuator slots     */
     static constexpr int CJ = TAU + NMS * ND;    /* phases 2-3: [NS][CJN] contact slots             */
     static constexpr int OBS = U;                /* report: observation staging                     */
-    static constexpr int U1 = 24 * NB + 6 * ND, U2 = NMS * ND + NS * CJN;
+    static constexpr int U1 = 24 * (NB + 1) + 6 * ND, U2 = NMS * ND + NS * CJN;
     static constexpr int USZ = U1 > U2 ? (U1 > BIOIM_OBS_MAX ? U1 : BIOIM_OBS_MAX) : (U2 > BIOIM_OBS_MAX ? U2 : BIOIM_OBS_MAX);
     static constexpr int SIZE = ((U + USZ + 1) / 2) * 2;
-};
-
-/* compile-time facts of a topology */
-template <class T> struct TopoInfo {
-    static constexpr unsigned axes_used() {
-        unsigned m = 0;
-        for (int c = 0; c < T::NB; ++c)
-            for (int a = 0; a < 6; ++a)
-                if (T::axis_kind[c * 6 + a] >= 0) m |= 1u << a;
-        return m;
-    }
-    static constexpr int depth() {
-        int d = 0;
-        for (int c = 0; c < T::NB; ++c) {
-            int l = 1;
-            for (int p = T::parent[c]; p >= 0; p = T::parent[p]) ++l;
-            d = l > d ? l : d;
-        }
-        return d;
-    }
 };
 
 DEV void wave_sync() {
@@ -359,13 +401,17 @@ DEV void kin_local(const SModel<T, Real> &SM, Real *lds, int c) {
         constexpr int ax = decltype(aI)::value;
         cd[ax] = -1;
         if constexpr (((USED >> ax) & 1u) != 0) {
+            constexpr unsigned KM = TopoInfo<T>::axis_kinds(ax);
             const int fi = b.fn[ax];
-            const int cc = fi >= 0 ? SM.fn[fi].coord : -1;
-            Real qc = 0, uc = 0;
-            if (cc >= 0) { qc = lds[LY::QF + cc]; uc = lds[LY::UF + cc]; }
+            const int fs = fi >= 0 ? fi : 0;
+            const int cc = fi >= 0 ? SM.fn[fs].coord : -1;
+            const int cs = cc >= 0 ? cc : 0;
+            Real qc = lds[LY::QF + cs], uc = lds[LY::UF + cs];
+            qc = cc >= 0 ? qc : Real(0);
+            uc = cc >= 0 ? uc : Real(0);
             Real f, f1, f2;
-            fn_eval<T, Real>(SM, fi, qc, f, f1, f2);
-            cd[ax] = cc >= 0 ? SM.coord_dof[cc] : -1;
+            fn_eval_km<KM, T, Real>(SM, fi, qc, f, f1, f2);
+            cd[ax] = cc >= 0 ? SM.coord_dof[cs] : -1;
             Real a[3] = {b.axis[ax][0], b.axis[ax][1], b.axis[ax][2]};
             if constexpr (ax < 3) {
                 Real ucol[3], cr[3];
@@ -449,90 +495,106 @@ DEV void kin_local(const SModel<T, Real> &SM, Real *lds, int c) {
     });
 }
 
-/* parent frame of body c's joint (ground: identity at the shifted origin) */
-template <class T, typename Real>
-DEV void parent_frame(const Real *lds, int p, Real x0, Real *RP, Real *oP) {
-    using LY = Lay<T, Real>;
-    const bool g = p < 0;
-    const Real *kp = lds + LY::KB + 18 * (g ? 0 : p);
-#pragma unroll
-    for (int i = 0; i < 9; ++i) RP[i] = g ? ((i % 4) == 0 ? Real(1) : Real(0)) : kp[i];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) oP[i] = g ? (i == 0 ? -x0 : Real(0)) : kp[9 + i];
-}
+/* body frame and motion: orientation, origin, angular velocity, spatial
+ * velocity at the (shifted) ground origin, and the velocity-product
+ * accelerations (zero q'') */
+template <typename Real> struct Frame {
+    Real R[9], o[3], w[3], vO[3], al[3], aO[3];
+};
 
-/* Phase 1b (lane = body at the current tree level): compose with the parent */
-template <class T, typename Real>
-DEV void kin_compose(const SModel<T, Real> &SM, Real *lds, int c, Real x0) {
-    using LY = Lay<T, Real>;
-    const int p = SM.body[c].parent;
-    const bool g = p < 0;
-    const Real *kp = lds + LY::KB + 18 * (g ? 0 : p), *ap = lds + LY::AL + 6 * (g ? 0 : p);
-    Real RP[9], oP[3], wP[3], vOP[3], alP[3], aOP[3];
-    parent_frame<T, Real>(lds, p, x0, RP, oP);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        wP[i] = g ? Real(0) : kp[12 + i]; vOP[i] = g ? Real(0) : kp[15 + i];
-        alP[i] = g ? Real(0) : ap[i]; aOP[i] = g ? Real(0) : ap[3 + i];
-    }
-    const Real *lc = lds + LY::LOC + 24 * c;
+/* F := F composed with the joint whose parent-frame data is lc (LOC slot) */
+template <typename Real> DEV void compose(Frame<Real> &F, const Real *lc) {
     Real R[9], oB[3], w[3], wrg[3], vrel[3], vO[3], al[3], t[3], t2[3], t3[3];
-    mm3(RP, lc, R);
-    mv3(RP, lc + 9, t);
+    mm3(F.R, lc, R);
+    mv3(F.R, lc + 9, t);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) oB[i] = oP[i] + t[i];
-    mv3(RP, lc + 12, wrg);
+    for (int i = 0; i < 3; ++i) oB[i] = F.o[i] + t[i];
+    mv3(F.R, lc + 12, wrg);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) w[i] = wP[i] + wrg[i];
-    mv3(RP, lc + 15, vrel);
+    for (int i = 0; i < 3; ++i) w[i] = F.w[i] + wrg[i];
+    mv3(F.R, lc + 15, vrel);
     cross3(wrg, oB, t);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) vO[i] = vOP[i] + vrel[i] - t[i];
-    mv3(RP, lc + 18, t);
-    cross3(wP, wrg, t2);
+    for (int i = 0; i < 3; ++i) vO[i] = F.vO[i] + vrel[i] - t[i];
+    mv3(F.R, lc + 18, t);
+    cross3(F.w, wrg, t2);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) al[i] = alP[i] + t2[i] + t[i];
-    /* acceleration of the B origin (zero q''): parent point acceleration
+    for (int i = 0; i < 3; ++i) al[i] = F.al[i] + t2[i] + t[i];
+    /* acceleration of the new origin: parent point acceleration
      * + Coriolis 2 wP x vrel + relative acceleration */
     Real vpt[3], aB[3], aa[3];
-    cross3(wP, oB, t);
+    cross3(F.w, oB, t);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) vpt[i] = vOP[i] + t[i];
-    cross3(alP, oB, t);
-    cross3(wP, vpt, t2);
-    cross3(wP, vrel, t3);
-    mv3(RP, lc + 21, aa);
+    for (int i = 0; i < 3; ++i) vpt[i] = F.vO[i] + t[i];
+    cross3(F.al, oB, t);
+    cross3(F.w, vpt, t2);
+    cross3(F.w, vrel, t3);
+    mv3(F.R, lc + 21, aa);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) aB[i] = aOP[i] + t[i] + t2[i] + Real(2) * t3[i] + aa[i];
-    Real vB[3], aO[3];
+    for (int i = 0; i < 3; ++i) aB[i] = F.aO[i] + t[i] + t2[i] + Real(2) * t3[i] + aa[i];
+    Real vB[3];
     cross3(w, oB, t);
 #pragma unroll
     for (int i = 0; i < 3; ++i) vB[i] = vO[i] + t[i];
     cross3(al, oB, t);
     cross3(w, vB, t2);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) aO[i] = aB[i] - t[i] - t2[i];
-    Real *kb = lds + LY::KB + 18 * c, *ab = lds + LY::AL + 6 * c;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) kb[i] = R[i];
+    for (int i = 0; i < 9; ++i) F.R[i] = R[i];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        kb[9 + i] = oB[i]; kb[12 + i] = w[i]; kb[15 + i] = vO[i];
-        ab[i] = al[i]; ab[3 + i] = aO[i];
+        F.aO[i] = aB[i] - t[i] - t2[i];
+        F.o[i] = oB[i]; F.w[i] = w[i]; F.vO[i] = vO[i]; F.al[i] = al[i];
     }
 }
 
-/* Phase 1c (lane = dof): ground Plucker column */
-template <class T, typename Real>
-DEV void kin_column(const SModel<T, Real> &SM, Real *lds, int d, Real x0) {
+/* identity joint (LOC slot NB) and the ground frame (KB/AL slot NB) */
+template <class T, typename Real> DEV void kin_ground(Real *lds, Real x0) {
     using LY = Lay<T, Real>;
-    const int p = SM.body[SM.dof_cb[d]].parent;
-    Real RP[9], oP[3], Sa[3], Sl[3], t[3];
-    parent_frame<T, Real>(lds, p, x0, RP, oP);
+    Real *lc = lds + LY::LOC + 24 * T::NB, *kb = lds + LY::KB + 18 * T::NB, *ab = lds + LY::AL + 6 * T::NB;
+#pragma unroll
+    for (int i = 0; i < 24; ++i) lc[i] = (i < 9 && (i % 4) == 0) ? Real(1) : Real(0);
+#pragma unroll
+    for (int i = 0; i < 18; ++i) kb[i] = (i < 9 && (i % 4) == 0) ? Real(1) : Real(0);
+    kb[9] = -x0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) ab[i] = 0;
+}
+
+/* Phase 1b (lane = body c): compose c's root-to-body joint chain in
+ * registers (front-padded with the identity joint, so every lane runs the
+ * same DEPTH compositions with no inter-lane dependency) */
+template <class T, typename Real>
+DEV void kin_chain(const SModel<T, Real> &SM, Real *lds, int c, Real x0) {
+    using LY = Lay<T, Real>;
+    Frame<Real> F;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) F.R[i] = (i % 4) == 0 ? Real(1) : Real(0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { F.o[i] = i == 0 ? -x0 : Real(0); F.w[i] = 0; F.vO[i] = 0; F.al[i] = 0; F.aO[i] = 0; }
+    sfor<0, TopoInfo<T>::depth()>([&](auto lI) {
+        constexpr int lvl = decltype(lI)::value;
+        compose(F, lds + LY::LOC + 24 * SM.chain[c][lvl]);
+    });
+    Real *kb = lds + LY::KB + 18 * c, *ab = lds + LY::AL + 6 * c;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) kb[i] = F.R[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        kb[9 + i] = F.o[i]; kb[12 + i] = F.w[i]; kb[15 + i] = F.vO[i];
+        ab[i] = F.al[i]; ab[3 + i] = F.aO[i];
+    }
+}
+
+/* Phase 1c (lane = dof): ground Plucker column from the parent frame */
+template <class T, typename Real>
+DEV void kin_column(const SModel<T, Real> &SM, Real *lds, int d) {
+    using LY = Lay<T, Real>;
+    const Real *kp = lds + LY::KB + 18 * SM.body[SM.dof_cb[d]].pslot;
+    Real Sa[3], Sl[3], t[3];
     const Real *sl = lds + LY::SL + 6 * d;
-    mv3(RP, sl, Sa);
-    mv3(RP, sl + 3, Sl);
-    cross3(Sa, oP, t);
+    mv3(kp, sl, Sa);
+    mv3(kp, sl + 3, Sl);
+    cross3(Sa, kp + 9, t);
     Real *S = lds + LY::S + 6 * d;
 #pragma unroll
     for (int i = 0; i < 3; ++i) { S[i] = Sa[i]; S[3 + i] = Sl[i] - t[i]; }
@@ -661,7 +723,7 @@ template <typename Real> DEV Real smooth_step_d(Real y0, Real y1, Real x0, Real 
  * the 3x3 implicit damping/stiffness block (h > 0), assembled per M entry
  * and per rhs row in phase 3. */
 template <class T, typename Real>
-DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, int s, Real h) {
+DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, const Real (&S)[Lay<T, Real>::ND][6], int s, Real h) {
     using LY = Lay<T, Real>;
     constexpr int ND = LY::ND;
     const int cb = SM.sph_cb[s], fo = SM.sph_force[s];
@@ -715,11 +777,10 @@ DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, int s, Real h) {
     cj[3 * ND + 2] = F[2];
 #pragma unroll
     for (int d = 0; d < ND; ++d) {
-        const Real *S = lds + LY::S + 6 * d;
         Real on = (mask >> d) & 1u ? Real(1) : Real(0), j[3];
-        cross3(S, P, j);
+        cross3(S[d], P, j);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) cj[3 * d + i] = on * (j[i] + S[3 + i]);
+        for (int i = 0; i < 3; ++i) cj[3 * d + i] = on * (j[i] + S[d][3 + i]);
     }
     Real cxx = 0, cxz = 0, cyy = 0, czz = 0;
     if (h > 0) {
@@ -826,9 +887,13 @@ DEV Real muscle_equilibrium(const SModel<T, Real> &SM, const SMuscle<Real> &mu, 
     return l;
 }
 
-/* path length and dL/dq of one muscle (frames and Plucker columns from LDS) */
+/* path length and dL/dq of one muscle.  Frames from LDS, Plucker columns
+ * from registers (loaded once per dynamics call).  Fixed trip count over
+ * the topology's maximum point count; only the point indices that can be
+ * conditional / moving (compile-time masks) carry that code. */
 template <class T, typename Real>
-DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const Real *lds, Real &L, Real *dLdq) {
+DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const Real *lds,
+                     const Real (&S)[Lay<T, Real>::ND][6], Real &L, Real *dLdq) {
     using LY = Lay<T, Real>;
     const Real *ldsq = lds + LY::QF;
     L = 0;
@@ -843,58 +908,65 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
         cross3(Pp, g, mo);
 #pragma unroll
         for (int d = 0; d < T::ND; ++d) {
-            const Real *S = lds + LY::S + 6 * d;
             Real on = (maskp >> d) & 1u ? Real(1) : Real(0);
-            dLdq[d] += on * (dot3(S, mo) + dot3(S + 3, g)) + (mdofp == d ? dot3(g, dPp) : Real(0));
+            dLdq[d] += on * (dot3(S[d], mo) + dot3(S[d] + 3, g)) + (mdofp == d ? dot3(g, dPp) : Real(0));
         }
     };
-    for (int j = 0; j < mu.npt; ++j) {
-        const DPathPt<Real> &pt = SM.pt[mu.pt_off + j];
-        if (pt.type == BIOIM_PT_COND) {
-            Real qc = ldsq[pt.cond_coord];
-            if (qc < pt.lo || qc > pt.hi) continue;
-        }
-        Real loc[3], dloc[3] = {0, 0, 0};
-        if (pt.type == BIOIM_PT_MOVING) {
-            Real ll[3], dl[3] = {0, 0, 0};
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                if (pt.fn[a] < 0) { ll[a] = pt.loc[a]; continue; }
-                Real f, f1, f2;
-                fn_eval<T, Real>(SM, pt.fn[a], ldsq[pt.mcoord], f, f1, f2);
-                ll[a] = f; dl[a] = f1;
+    const int npt = mu.npt;
+    sfor<0, (T::MAXPT > 0 ? T::MAXPT : 1)>([&](auto jI) {
+        constexpr int j = decltype(jI)::value;
+        if (j < npt) {
+            const DPathPt<Real> &pt = SM.pt[mu.pt_off + j];
+            bool on = true;
+            if constexpr (((T::PT_COND >> j) & 1u) != 0) {
+                if (pt.type == BIOIM_PT_COND) {
+                    Real qc = ldsq[pt.cond_coord];
+                    on = !(qc < pt.lo || qc > pt.hi);
+                }
             }
-            mv3(pt.R, ll, loc);
+            if (on) {
+                Real loc[3] = {pt.loc[0], pt.loc[1], pt.loc[2]}, dloc[3] = {0, 0, 0};
+                if constexpr (((T::PT_MOVING >> j) & 1u) != 0) {
+                    if (pt.type == BIOIM_PT_MOVING) {
+                        Real ll[3], dl[3] = {0, 0, 0};
 #pragma unroll
-            for (int i = 0; i < 3; ++i) loc[i] += pt.p[i];
-            mv3(pt.R, dl, dloc);
-        } else {
+                        for (int a = 0; a < 3; ++a) {
+                            Real f, f1, f2;
+                            fn_eval<T, Real>(SM, pt.fn[a], ldsq[pt.mcoord], f, f1, f2);
+                            ll[a] = pt.fn[a] < 0 ? pt.loc[a] : f;
+                            dl[a] = pt.fn[a] < 0 ? Real(0) : f1;
+                        }
+                        mv3(pt.R, ll, loc);
 #pragma unroll
-            for (int i = 0; i < 3; ++i) loc[i] = pt.loc[i];
+                        for (int i = 0; i < 3; ++i) loc[i] += pt.p[i];
+                        mv3(pt.R, dl, dloc);
+                    }
+                }
+                const Real *Rb = lds + LY::KB + 18 * pt.cbody;
+                Real P[3], dP[3];
+                mv3(Rb, loc, P);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) P[i] += Rb[9 + i];
+                mv3(Rb, dloc, dP);
+                Real e[3] = {0, 0, 0};
+                if (have) {
+                    Real sgm[3] = {P[0] - Pp[0], P[1] - Pp[1], P[2] - Pp[2]};
+                    Real len = sqrt(dot3(sgm, sgm));
+                    L += len;
+                    Real inv = Real(1) / len;
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) e[a] = sgm[a] * inv;
+                    Real g[3] = {ep[0] - e[0], ep[1] - e[1], ep[2] - e[2]};
+                    flush(g);
+                }
+#pragma unroll
+                for (int a = 0; a < 3; ++a) { ep[a] = e[a]; Pp[a] = P[a]; dPp[a] = dP[a]; }
+                maskp = pt.dofmask;
+                mdofp = pt.mdof;
+                have = true;
+            }
         }
-        const Real *Rb = lds + LY::KB + 18 * pt.cbody;
-        Real P[3], dP[3];
-        mv3(Rb, loc, P);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) P[i] += Rb[9 + i];
-        mv3(Rb, dloc, dP);
-        Real e[3] = {0, 0, 0};
-        if (have) {
-            Real sgm[3] = {P[0] - Pp[0], P[1] - Pp[1], P[2] - Pp[2]};
-            Real len = sqrt(dot3(sgm, sgm));
-            L += len;
-            Real inv = Real(1) / len;
-#pragma unroll
-            for (int a = 0; a < 3; ++a) e[a] = sgm[a] * inv;
-            Real g[3] = {ep[0] - e[0], ep[1] - e[1], ep[2] - e[2]};
-            flush(g);
-        }
-#pragma unroll
-        for (int a = 0; a < 3; ++a) { ep[a] = e[a]; Pp[a] = P[a]; dPp[a] = dP[a]; }
-        maskp = pt.dofmask;
-        mdofp = pt.mdof;
-        have = true;
-    }
+    });
     if (have) flush(ep);
 }
 
@@ -916,6 +988,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
                   Real control, int lane, Real *lds, Real h, bool equilibrate, Dyn<T, Real> &D) {
     using LY = Lay<T, Real>;
     constexpr int ND = LY::ND, NP = LY::NP, NB = T::NB, G = T::G;
+    static_assert(NB < G && ND <= G, "lane NB writes the ground slot; one lane per dof");
     STAMP_DECL
     Real x0 = 0;
     if constexpr (T::TX >= 0) {
@@ -937,17 +1010,21 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
 
     /* ---- phase 1: lane-parallel kinematics */
     if (lane < NB) kin_local<T, Real>(SM, lds, lane);
+    if (lane == NB) kin_ground<T, Real>(lds, x0);
     wave_sync();
     STAMP(0);
-    sfor<0, TopoInfo<T>::depth()>([&](auto lI) {
-        constexpr int lvl = decltype(lI)::value;
-        if (lane < NB && SM.body[lane].level == lvl) kin_compose<T, Real>(SM, lds, lane, x0);
-        wave_sync();
-    });
+    if (lane < NB) kin_chain<T, Real>(SM, lds, lane, x0);
+    wave_sync();
     STAMP(1);
-    if (lane < ND) kin_column<T, Real>(SM, lds, lane, x0);
+    if (lane < ND) kin_column<T, Real>(SM, lds, lane);
     if (lane < NB) body_inertia<T, Real>(SM, M, lds, lane);
     wave_sync();
+    /* Plucker columns in registers for the muscle-path and contact lanes */
+    Real Sr[ND][6];
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) Sr[d][i] = lds[LY::S + 6 * d + i];
     STAMP(2);
 
     /* ---- phase 2: lane-parallel force elements */
@@ -972,7 +1049,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
         if (lane < T::NM) {
             const SMuscle<Real> &mu = SM.mus[lane];
             Real L, dLdq[ND];
-            muscle_path<T, Real>(SM, mu, lds, L, dLdq);
+            muscle_path<T, Real>(SM, mu, lds, Sr, L, dLdq);
             STAMP(4);
             if (equilibrate) { /* reset: default activation, static fiber equilibrium */
                 act = mu.default_act;
@@ -993,7 +1070,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
         }
     }
     STAMP(5);
-    if (lane < T::NS) contact_lane<T, Real>(SM, lds, lane, h);
+    if (lane < T::NS) contact_lane<T, Real>(SM, lds, Sr, lane, h);
     STAMP(6);
     if (lane < T::NL) {
         int cc = SM.lim_coord[lane];
@@ -1663,9 +1740,11 @@ template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, 
         d.mass = (Real)b.mass;
         for (int i = 0; i < 6; ++i) d.inertia[i] = (Real)b.inertia[i];
         d.parent = b.parent;
-        int lvl = 0;
-        for (int q = b.parent; q >= 0; q = p.cbody[q].parent) ++lvl;
-        d.level = lvl;
+        d.pslot = b.parent >= 0 ? b.parent : T::NB;
+        constexpr int DEP = TopoInfo<T>::depth();
+        int path[DEP], n = 0;
+        for (int q = c; q >= 0 && n < DEP; q = p.cbody[q].parent) path[n++] = q;
+        for (int l = 0; l < DEP; ++l) m.chain[c][l] = l < DEP - n ? T::NB : path[DEP - 1 - l];
     }
     for (int f = 0; f < p.nfn; ++f) {
         m.fn[f].type = p.fn[f].type; m.fn[f].coord = p.fn[f].coord; m.fn[f].off = p.fn[f].knot_off;

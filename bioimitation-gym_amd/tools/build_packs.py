@@ -121,6 +121,16 @@ def emit_topology(struct, pk, lanes):
     s += f'    static constexpr int NPT = {pk.npathpt}, NFN = {pk.nfn}, NKNOT = {pk.nknots},' \
          f' NCURVE = {len(unique_curves(pk))},' \
          f' NKMAX = {max([pk.fn[i].nknots for i in range(pk.nfn)] + [2])};\n'
+    maxpt, cond, move = 0, 0, 0
+    for i in range(pk.nmuscle):
+        m = pk.muscle[i]
+        maxpt = max(maxpt, m.npt)
+        for j in range(m.npt):
+            t = pk.pathpt[m.pt_off + j].type
+            cond |= (1 << j) if t == 1 else 0
+            move |= (1 << j) if t == 2 else 0
+    s += f'    static constexpr int MAXPT = {maxpt}; /* path points per muscle (max) */\n'
+    s += f'    static constexpr unsigned PT_COND = {cond}u, PT_MOVING = {move}u; /* point indices that can be conditional / moving */\n'
     s += f'    static constexpr int TX = {pk.coord_tx}, TY = {pk.coord_ty}, TZ = {pk.coord_tz};\n'
     s += f'    static constexpr int TORSO = {pk.torso_body}, CALCN_R = {pk.calcn_r_body}, CALCN_L = {pk.calcn_l_body};\n'
     s += f'    static constexpr unsigned FLAGS = {pk.env_flags & 0x9f}u; /* structural env flags */\n'
