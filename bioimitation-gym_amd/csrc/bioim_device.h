@@ -120,6 +120,11 @@ struct SModel {
     int32_t coord_dof[D::NCD], dof_cb[D::NDD];
     int32_t e_l[D::NP], e_k[D::NP], e_c[D::NP]; /* packed-lower M entry -> (row, col, subtree body) */
     uint32_t dofmask[T::NB];
+    /* OpenSim bodies reported in observations / rewards (lane = body) */
+    Real os_p[T::NOS][3];
+    int32_t os_cb[T::NOS];
+    int32_t obs_slot[T::NOBP + T::NOBV]; /* report slots of the observed bodies (NOS = COM) */
+    int32_t rw_slot[BIOIM_NREFBODY];     /* report slots of the reward's reference bodies  */
     /* root-to-body joint chain, front-padded with the identity joint slot NB */
     int32_t chain[T::NB][TopoInfo<T>::depth()];
     int32_t sph_cb[D::NSD], sph_force[D::NSD], lim_coord[D::NLD], lim_dof[D::NLD], act_dof[D::NAD];

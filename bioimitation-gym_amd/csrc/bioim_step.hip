@@ -339,8 +339,10 @@ template <class T, typename Real> struct Lay {
     static constexpr int TAU = U;                /* phases 2-3: [NMS][ND] muscle/actuator slots     */
     static constexpr int CJ = TAU + NMS * ND;    /* phases 2-3: [NS][CJN] contact slots             */
     static constexpr int OBS = U;                /* report: observation staging                     */
+    static constexpr int REP = OBS + BIOIM_OBS_MAX; /* report: [NOS+1][6] body pos/vel (NOS: COM) */
     static constexpr int U1 = 24 * (NB + 1) + 6 * ND, U2 = NMS * ND + NS * CJN;
-    static constexpr int USZ = U1 > U2 ? (U1 > BIOIM_OBS_MAX ? U1 : BIOIM_OBS_MAX) : (U2 > BIOIM_OBS_MAX ? U2 : BIOIM_OBS_MAX);
+    static constexpr int U3 = BIOIM_OBS_MAX + 6 * (T::NOS + 1);
+    static constexpr int USZ = U1 > U2 ? (U1 > U3 ? U1 : U3) : (U2 > U3 ? U2 : U3);
     static constexpr int SIZE = ((U + USZ + 1) / 2) * 2;
 };
 
@@ -1158,43 +1160,58 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
     STAMP(9);
 }
 
-/* body origin position/velocity of OpenSim body OB (-1 = system COM), in
- * absolute ground coordinates, from the published frames */
-template <class T, int OB, typename Real>
-DEV void report_body(const DModel<Real> &M, const Real *lds, Real x0, Real *pos, Real *vel) {
+/* Lane-parallel report (lane = OpenSim body b < NOS; lane NOS = system
+ * COM): origin position and velocity in absolute ground coordinates, from
+ * the published frames, into REP[b] */
+template <class T, typename Real>
+DEV void report_points(const SModel<T, Real> &SM, Real *lds, int lane, Real x0) {
     using LY = Lay<T, Real>;
-    if constexpr (OB >= 0) {
-        constexpr int c = T::os_cb[OB];
-        const Real *kb = lds + LY::KB + 18 * c;
-        mv3(kb, M.os_p[OB], pos);
+    static_assert(T::NOS < T::G, "one lane per reported body plus one for the COM");
+    Real pos[3], vel[3], t[3];
+    if (lane < T::NOS) {
+        const Real *kb = lds + LY::KB + 18 * SM.os_cb[lane];
+        mv3(kb, SM.os_p[lane], pos);
 #pragma unroll
         for (int i = 0; i < 3; ++i) pos[i] += kb[9 + i];
-        Real t[3];
         cross3(kb + 12, pos, t);
 #pragma unroll
         for (int i = 0; i < 3; ++i) vel[i] = kb[15 + i] + t[i];
     } else {
         Real mt = 0, cs[3] = {0, 0, 0}, vs[3] = {0, 0, 0};
-        sfor<0, T::NB>([&](auto cI) {
-            constexpr int c = decltype(cI)::value;
+#pragma unroll
+        for (int c = 0; c < T::NB; ++c) {
             const Real *kb = lds + LY::KB + 18 * c;
-            Real cG[3], vc[3], t[3];
-            mv3(kb, M.com[c], cG);
+            Real cG[3], vc[3];
+            mv3(kb, SM.body[c].com, cG);
 #pragma unroll
             for (int i = 0; i < 3; ++i) cG[i] += kb[9 + i];
             cross3(kb + 12, cG, t);
 #pragma unroll
             for (int i = 0; i < 3; ++i) vc[i] = kb[15 + i] + t[i];
-            Real m = M.mass[c];
+            Real m = SM.body[c].mass;
 #pragma unroll
             for (int i = 0; i < 3; ++i) { cs[i] += m * cG[i]; vs[i] += m * vc[i]; }
             mt += m;
-        });
+        }
 #pragma unroll
         for (int i = 0; i < 3; ++i) { pos[i] = cs[i] / mt; vel[i] = vs[i] / mt; }
     }
     pos[0] += x0;
+    Real *r = lds + LY::REP + 6 * (lane < T::NOS ? lane : T::NOS);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { r[i] = pos[i]; r[3 + i] = vel[i]; }
 }
+
+/* REP slot of an OpenSim body index (-1 = COM) */
+template <class T> DEV constexpr int rep_slot(int ob) { return ob >= 0 ? ob : T::NOS; }
+
+/* observation offsets (get_state_dict order, muscle_walking_imitation_env2D.py:158-225) */
+template <class T> struct ObsLayout {
+    static constexpr int NTR = (T::TX >= 0) + (T::TY >= 0) + (T::TZ >= 0);
+    static constexpr int NQ = T::NC - NTR;
+    static constexpr int QPOS = 1, QVEL = QPOS + NQ, QACC = QVEL + T::NC, TGT = QACC + T::NC;
+    static constexpr int body(bool tgt) { return TGT + (tgt ? 2 * (T::NC - 1) : 0); }
+};
 
 DEV int clamp_row(int r, int nrows) { return r < 0 ? 0 : (r >= nrows ? nrows - 1 : r); }
 
@@ -1378,84 +1395,73 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
             pending_reset = false;
             reported_reset = true;
         }
-        /* ---- realized state: observation */
+        /* ---- realized state: observation (lane-parallel; get_state_dict,
+         * muscle_walking_imitation_env2D.py:158-225).  The realize call left
+         * the coordinates (QF/UF), frames (KB), contact wrenches (CW) and limit
+         * forces (LIM) in LDS; report points first. */
+        using OL = ObsLayout<T>;
         const Real x0 = D.x0;
         Real *ob = lds + LY::OBS;
         const bool tgt = (M.env_flags & BIOIM_ENV_TARGET_OBS) != 0, grf = (M.env_flags & BIOIM_ENV_GRF_OBS) != 0;
-        Real qdd_f[T::NC], qf[T::NC], uf[T::NC];
-        fill_coords<T, Real>(M, q, u, qf, uf);
-        sfor<0, T::NC>([&](auto cI) {
-            constexpr int c = decltype(cI)::value;
-            constexpr int d = T::coord_dof[c];
-            if constexpr (d >= 0) qdd_f[c] = D.qdd[d]; else qdd_f[c] = 0;
-        });
-        Real px = qf[T::TX], py = qf[T::TY];
+        if (lane <= T::NOS) report_points<T, Real>(SM, lds, lane, x0);
+        wave_sync();
+        const Real px = lds[LY::QF + T::TX], py = lds[LY::QF + T::TY];
         Real pz = 0;
-        if constexpr (T::TZ >= 0) pz = qf[T::TZ];
+        if constexpr (T::TZ >= 0) pz = lds[LY::QF + T::TZ];
         if (lane == 0) {
-            int k = 0;
             double ph = (double)istep / (double)M.cycle;
-            ob[k++] = Real(ph - floor(ph));
-            sfor<0, T::NC>([&](auto cI) {
-                constexpr int c = decltype(cI)::value;
-                if constexpr (c != T::TX && c != T::TY && c != T::TZ) ob[k++] = qf[c];
-            });
+            ob[0] = Real(ph - floor(ph));
+        }
+        const int obody = OL::body(tgt);
+        if (lane < T::NC) {
+            const int c = lane;
+            const bool trans = c == T::TX || c == T::TY || c == T::TZ;
+            const int qi = c - (T::TX >= 0 && T::TX < c) - (T::TY >= 0 && T::TY < c) - (T::TZ >= 0 && T::TZ < c);
+            if (!trans) ob[OL::QPOS + qi] = lds[LY::QF + c];
+            ob[OL::QVEL + c] = lds[LY::UF + c];
+            const int dc = SM.coord_dof[c];
+            Real acc = 0;
 #pragma unroll
-            for (int c = 0; c < T::NC; ++c) ob[k++] = uf[c];
-#pragma unroll
-            for (int c = 0; c < T::NC; ++c) ob[k++] = qdd_f[c];
-            if (tgt) {
-                int r = clamp_row(istep + 1, M.nrows);
-#pragma unroll
-                for (int c = 0; c < T::NC; ++c)
-                    if (c != T::TX) ob[k++] = M.ref_q[r][c];
-#pragma unroll
-                for (int c = 0; c < T::NC; ++c)
-                    if (c != T::TX) ob[k++] = M.ref_u[r][c];
-            }
-            sfor<0, T::NOBP>([&](auto bI) {
-                constexpr int b = decltype(bI)::value;
-                Real p3[3], v3[3];
-                report_body<T, T::obs_bpos[b], Real>(M, lds, x0, p3, v3);
-                ob[k++] = p3[0] - px; ob[k++] = p3[1] - py; ob[k++] = p3[2] - pz;
-            });
-            sfor<0, T::NOBV>([&](auto bI) {
-                constexpr int b = decltype(bI)::value;
-                Real p3[3], v3[3];
-                report_body<T, T::obs_bvel[b], Real>(M, lds, x0, p3, v3);
-                ob[k++] = v3[0]; ob[k++] = v3[1]; ob[k++] = v3[2];
-            });
-            k += 3 * NM;
-            if (grf) {
-                sfor<0, T::NF>([&](auto fI) {
-                    constexpr int f = decltype(fI)::value;
-                    Real F[3] = {0, 0, 0}, Mo[3] = {0, 0, 0};
-                    sfor<0, T::NS>([&](auto sI) {
-                        constexpr int s2 = decltype(sI)::value;
-                        if constexpr (T::sphere_force[s2] == f) {
-                            const Real *cw = lds + LY::CW + 8 * s2;
-#pragma unroll
-                            for (int i = 0; i < 3; ++i) { F[i] += cw[i]; Mo[i] += cw[3 + i]; }
-                        }
-                    });
-                    /* moments about the absolute ground origin: (x0,0,0) x F */
-                    Mo[1] += -x0 * F[2];
-                    Mo[2] += x0 * F[1];
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) ob[k++] = F[i] / M.weight;
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) ob[k++] = Mo[i] / M.moment;
-                });
+            for (int d = 0; d < ND; ++d) acc = dc == d ? D.qdd[d] : acc;
+            ob[OL::QACC + c] = acc;
+            if (tgt && c != T::TX) {
+                const int r1 = clamp_row(istep + 1, M.nrows), ti = c - (T::TX >= 0 && T::TX < c);
+                ob[OL::TGT + ti] = M.ref_q[r1][c];
+                ob[OL::TGT + (T::NC - 1) + ti] = M.ref_u[r1][c];
             }
         }
+        if (lane < T::NOBP) {
+            const Real *rp = lds + LY::REP + 6 * SM.obs_slot[lane];
+            ob[obody + 3 * lane] = rp[0] - px; ob[obody + 3 * lane + 1] = rp[1] - py; ob[obody + 3 * lane + 2] = rp[2] - pz;
+        }
+        if (lane < T::NOBV) {
+            const Real *rp = lds + LY::REP + 6 * SM.obs_slot[T::NOBP + lane];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) ob[obody + 3 * T::NOBP + 3 * lane + i] = rp[3 + i];
+        }
+        const int omus = obody + 3 * T::NOBP + 3 * T::NOBV;
         if constexpr (NM > 0) {
-            int mb = 1 + (T::NC - (T::TX >= 0) - (T::TY >= 0) - (T::TZ >= 0)) + 2 * T::NC +
-                     (tgt ? 2 * (T::NC - 1) : 0) + 3 * T::NOBP + 3 * T::NOBV;
             if (lane < NM) {
-                ob[mb + 3 * lane] = D.ms.act;
-                ob[mb + 3 * lane + 1] = D.ms.lce;
-                ob[mb + 3 * lane + 2] = D.ms.vce;
+                ob[omus + 3 * lane] = D.ms.act;
+                ob[omus + 3 * lane + 1] = D.ms.lce;
+                ob[omus + 3 * lane + 2] = D.ms.vce;
             }
+        }
+        if (grf && lane < T::NF) {
+            Real F[3] = {0, 0, 0}, Mo[3] = {0, 0, 0};
+#pragma unroll
+            for (int s2 = 0; s2 < T::NS; ++s2) {
+                const Real *cw = lds + LY::CW + 8 * s2;
+                const bool mine = SM.sph_force[s2] == lane;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) { F[i] += mine ? cw[i] : Real(0); Mo[i] += mine ? cw[3 + i] : Real(0); }
+            }
+            /* moments about the absolute ground origin: (x0,0,0) x F */
+            Mo[1] += -x0 * F[2];
+            Mo[2] += x0 * F[1];
+            const int og = omus + 3 * NM + 6 * lane;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { ob[og + i] = F[i] / M.weight; ob[og + 3 + i] = Mo[i] / M.moment; }
         }
         wave_sync();
         if (obs)
@@ -1463,33 +1469,35 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
         wave_sync();
         if (reported_reset) break;
 
-        /* ---- reward (get_reward) and termination (is_done) */
+        /* ---- reward (get_reward) and termination (is_done); group sums are
+         * xor butterflies, so every lane holds bitwise-identical totals */
         {
-            int r = clamp_row(istep, M.nrows);
-            Real qerr = 0;
-#pragma unroll
-            for (int c = 0; c < T::NC; ++c) {
-                Real e = qf[c] - M.ref_q[r][c];
-                qerr += e * e;
+            const int r = clamp_row(istep, M.nrows);
+            Real e2 = 0;
+            if (lane < T::NC) {
+                Real e = lds[LY::QF + lane] - M.ref_q[r][lane];
+                e2 = e * e;
             }
-            qerr /= Real(T::NC);
-            Real err[BIOIM_NREFBODY];
-            sfor<0, BIOIM_NREFBODY>([&](auto bI) {
-                constexpr int b = decltype(bI)::value;
-                Real p3[3], v3[3];
-                report_body<T, T::rw_body[b], Real>(M, lds, x0, p3, v3);
-                Real s2 = 0;
+            const Real qerr = group_sum<G>(e2) / Real(T::NC);
+            Real eb = 0;
+            if (lane < BIOIM_NREFBODY) {
+                const Real *rp = lds + LY::REP + 6 * SM.rw_slot[lane];
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
-                    Real e = p3[i] - M.ref_x[r][b][i];
-                    s2 += e * e;
+                    Real e = rp[i] - M.ref_x[r][lane][i];
+                    eb += e * e;
                 }
-                err[b] = s2 / Real(3);
-            });
+                eb /= Real(3);
+            }
+            /* rw bodies: 0 COM, 1/2 femur r/l, 3/4 tibia, 5/6 talus, 7/8 calcn */
+            const bool odd = (lane & 1) != 0 && lane < BIOIM_NREFBODY, even = (lane & 1) == 0 && lane > 0 && lane < BIOIM_NREFBODY;
+            const Real err_com = group_sum<G>(lane == 0 ? eb : Real(0));
+            const Real err_r = group_sum<G>(odd ? eb : Real(0));
+            const Real err_l = group_sum<G>(even ? eb : Real(0));
             Real position_r = exp(Real(-30) * qerr);
-            Real com_r = exp(Real(-20) * err[0]);
-            Real foot_r = Real(0.5) * exp(Real(-20) * (err[7] + err[1] + err[3] + err[5]));
-            Real foot_l = Real(0.5) * exp(Real(-20) * (err[8] + err[2] + err[4] + err[6]));
+            Real com_r = exp(Real(-20) * err_com);
+            Real foot_r = Real(0.5) * exp(Real(-20) * err_r);
+            Real foot_l = Real(0.5) * exp(Real(-20) * err_l);
             Real pelvis_x = px;
             Real da = lane < NA ? curr - last : Real(0);
             Real action_r = exp(-M.action_r_scale * sqrt(group_sum<G>(da * da)));
@@ -1501,8 +1509,11 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
                 if (lane < NM) {
                     const SMuscle<Real> &mu = SM.mus[lane];
                     Real l = mu.slow, ex = control, aa = D.ms.act, hp = Real(0.5 * 3.14159265358979323846);
-                    Real fa = Real(40) * l * sin(hp * ex) + Real(133) * (Real(1) - l) * (Real(1) - cos(hp * ex));
-                    Real fm = Real(74) * l * sin(hp * aa) + Real(111) * (Real(1) - l) * (Real(1) - cos(hp * aa));
+                    Real se, ce, sa, ca;
+                    sincos_rt(hp * ex, se, ce);
+                    sincos_rt(hp * aa, sa, ca);
+                    Real fa = Real(40) * l * se + Real(133) * (Real(1) - l) * (Real(1) - ce);
+                    Real fm = Real(74) * l * sa + Real(111) * (Real(1) - l) * (Real(1) - ca);
                     Real ln = D.ms.lce * mu.inv_lopt, vv = D.ms.vce;
                     Real g = 0;
                     if (ln < Real(0.5)) g = Real(0.5);
@@ -1525,25 +1536,20 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
             inf[0] = position_r; inf[1] = com_r; inf[2] = foot_l; inf[3] = foot_r; inf[4] = a_error;
             last = curr;
             old_px = pelvis_x;
-            /* is_done */
-            Real p3[3], v3[3];
-            report_body<T, T::TORSO, Real>(M, lds, x0, p3, v3);
+            /* is_done (muscle_walking_imitation_env2D.py:237-265) */
+            const Real torso_y = lds[LY::REP + 6 * T::TORSO + 1];
             Real lmax = 0, amax = 0;
 #pragma unroll
             for (int li = 0; li < T::NL; ++li) lmax = fmax(lmax, fabs(lds[LY::LIM + 4 * li]));
 #pragma unroll
-            for (int c = 0; c < T::NC; ++c)
-                if (T::coord_dof[c] >= 0) amax = fmax(amax, fabs(qdd_f[c]));
+            for (int d = 0; d < ND; ++d) amax = fmax(amax, fabs(D.qdd[d]));
             int d_ = 0;
-            if (p3[1] < M.torso_y_min) d_ = 1;
+            if (torso_y < M.torso_y_min) d_ = 1;
             else if (lmax > M.limit_force_max) d_ = 1;
             else if (amax > M.acc_max) d_ = 1;
             else if (istep >= M.n_episode) d_ = 1;
             else if constexpr ((T::FLAGS & BIOIM_ENV_DONE_CROSS) != 0) {
-                Real pr[3], pl[3];
-                report_body<T, T::CALCN_R, Real>(M, lds, x0, pr, v3);
-                report_body<T, T::CALCN_L, Real>(M, lds, x0, pl, v3);
-                if (pr[2] - pl[2] < 0) d_ = 1;
+                if (lds[LY::REP + 6 * T::CALCN_R + 2] - lds[LY::REP + 6 * T::CALCN_L + 2] < 0) d_ = 1;
             }
 #pragma unroll
             for (int d = 0; d < ND; ++d)
@@ -1782,6 +1788,13 @@ template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, 
     for (int c = 0; c < p.ncoord; ++c)
         if (p.coord[c].dof >= 0) m.dof_cb[p.coord[c].dof] = p.coord[c].cbody;
     for (int c = 0; c < T::NB; ++c) m.dofmask[c] = T::dofmask[c];
+    for (int b = 0; b < T::NOBP; ++b) m.obs_slot[b] = T::obs_bpos[b] >= 0 ? T::obs_bpos[b] : T::NOS;
+    for (int b = 0; b < T::NOBV; ++b) m.obs_slot[T::NOBP + b] = T::obs_bvel[b] >= 0 ? T::obs_bvel[b] : T::NOS;
+    for (int b = 0; b < BIOIM_NREFBODY; ++b) m.rw_slot[b] = T::rw_body[b] >= 0 ? T::rw_body[b] : T::NOS;
+    for (int b = 0; b < T::NOS; ++b) {
+        m.os_cb[b] = p.osbody[b].cbody;
+        for (int i = 0; i < 3; ++i) m.os_p[b][i] = (Real)p.osbody[b].p[i];
+    }
     for (int l = 0, e = 0; l < p.ndof; ++l)
         for (int k = 0; k <= l; ++k, ++e) {
             int cl = m.dof_cb[l], ck = m.dof_cb[k];
