@@ -1,0 +1,178 @@
+"""Reference-shaped single-environment API.
+
+Drop-in for the reference's task-env classes: ``Env(config)`` with
+``reset(obs_as_dict=False)`` / ``step(action, obs_as_dict=False)`` returning
+``[obs, reward, done, {'all_rewards': [...]}]``, gym-style ``action_space`` /
+``observation_space`` / ``spec.timestep_limit`` and a no-op ``render``
+(opensim_environment.py:33-113, muscle_walking_imitation_env2D.py:18-403,
+torque_walking_imitation_env2D.py:18-366).  Every instance is one env of a
+:class:`~bioimitation.vector_env.VectorEnv` on the GPU: the physics runs in
+the HIP kernel, never on the host.  For throughput, step many envs at once
+with ``VectorEnv`` directly.
+
+Reset-index semantics follow the reference exactly: ``random.randint(0, N/2)``
+from Python's ``random`` module in train mode (so ``random.seed`` reproduces
+the reference's choice), index 0 in test mode
+(muscle_walking_imitation_env2D.py:133-156).
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+
+from .registry import REGISTERED_IDS, RECIPES, load_pack
+
+DEFAULT_CONFIG = {  # configs/env_default.py keys the envs read
+    'mode': 'train', 'visualize': False, 'max_actuation': 200.0, 'log': False,
+    'r_weights': [0.8, 0.2, 0.1], 'horizon': 5, 'use_target_obs': True, 'use_GRF': True,
+    'apply_perturbations': False,
+}
+
+
+class Box:
+    """Minimal gym.spaces.Box stand-in (used when gym is not installed)."""
+
+    def __init__(self, low, high, dtype=np.float64):
+        self.low = np.asarray(low, dtype=dtype)
+        self.high = np.asarray(high, dtype=dtype)
+        self.shape = self.low.shape
+        self.dtype = np.dtype(dtype)
+
+    def sample(self, rng=None):
+        rng = rng or np.random.default_rng()
+        lo = np.where(np.isfinite(self.low), self.low, -1.0)
+        hi = np.where(np.isfinite(self.high), self.high, 1.0)
+        return rng.uniform(lo, hi).astype(self.dtype)
+
+    def contains(self, x):
+        x = np.asarray(x)
+        return x.shape == self.shape and bool(np.all(x >= self.low) and np.all(x <= self.high))
+
+    def __repr__(self):
+        return f'Box({self.shape})'
+
+
+def _box(low, high):
+    try:
+        from gym import spaces
+        return spaces.Box(np.array(low), np.array(high))
+    except Exception:
+        return Box(low, high)
+
+
+class Specification:
+    """opensim_environment.py:9-13"""
+
+    def __init__(self, timestep_limit):
+        self.id = 0
+        self.timestep_limit = timestep_limit
+
+
+class ImitationEnv:
+    """One environment of a registered ID on one GPU (see module docstring)."""
+    env_id = None
+
+    def __init__(self, config=None, device=0, precision=64, seed=0):
+        cfg = dict(DEFAULT_CONFIG)
+        cfg.update(config or {})
+        if cfg.get('apply_perturbations'):
+            raise NotImplementedError('apply_perturbations (torso PrescribedForce) is not part of the HIP step')
+        from .vector_env import VectorEnv
+        self.config = cfg
+        self.test = cfg.get('mode') == 'test'
+        self._env = VectorEnv(self.env_id, 1, config=cfg, device=device, precision=precision, seed=seed,
+                              auto_reset=False)
+        pk = self._env.pack
+        self.N = pk.n_episode
+        self.cycle = pk.cycle
+        if pk.nmuscle:
+            lo, hi = [0.0] * pk.nact, [1.0] * pk.nact
+        else:
+            lo = [pk.coordact[a].min_control for a in range(pk.nact)]
+            hi = [pk.coordact[a].max_control for a in range(pk.nact)]
+        self.action_space = _box(lo, hi)
+        n = self._env.obs_dim
+        self.observation_space = _box([-np.inf] * n, [np.inf] * n)
+        self.timestep_limit = 1e10
+        self.spec = Specification(self.timestep_limit)
+        self.spec.action_space = self.action_space
+        self.spec.observation_space = self.observation_space
+
+    # -- reference API -------------------------------------------------------
+    def reset(self, obs_as_dict=False):
+        if obs_as_dict:
+            raise NotImplementedError('obs_as_dict: the observation is assembled flat on the GPU')
+        index = 0 if self.test else random.randint(0, int(self.N / 2))
+        obs = self._env.reset(env_ids=[0], ref_index=[index])
+        return obs[0].double().cpu().numpy()
+
+    def step(self, action, obs_as_dict=False):
+        if obs_as_dict:
+            raise NotImplementedError('obs_as_dict: the observation is assembled flat on the GPU')
+        import torch
+        a = torch.as_tensor(np.asarray(action, dtype=np.float64).reshape(1, -1), dtype=self._env.dtype,
+                            device=self._env.device)
+        obs, rew, done, info = self._env.step(a)
+        info = info[0].double().cpu().numpy()
+        return [obs[0].double().cpu().numpy(), float(rew[0]), bool(done[0]),
+                {'all_rewards': [float(v) for v in info]}]
+
+    def render(self, mode='human', close=False):
+        return
+
+    def get_observation_space_size(self):
+        return self._env.obs_dim
+
+    def get_action_space_size(self):
+        return self._env.action_dim
+
+    def seed(self, s=None):
+        random.seed(s)
+        return [s]
+
+    def close(self):
+        self._env.close()
+
+
+class MuscleWalkingImitationEnv2D(ImitationEnv):
+    env_id = 'MuscleWalkingImitation2D-v0'
+
+
+class TorqueWalkingImitationEnv2D(ImitationEnv):
+    env_id = 'TorqueWalkingImitation2D-v0'
+
+
+ENV_CLASSES = {c.env_id: c for c in (MuscleWalkingImitationEnv2D, TorqueWalkingImitationEnv2D)}
+
+
+def make(env_id, config=None, **kw):
+    """Construct the env class registered under ``env_id``."""
+    if env_id not in ENV_CLASSES:
+        if env_id in REGISTERED_IDS:
+            raise NotImplementedError(f'{env_id} is registered by the reference but not built yet')
+        raise KeyError(env_id)
+    return ENV_CLASSES[env_id](config, **kw)
+
+
+def register_with_gym():
+    """gym.register / ray register_env for the built IDs when those packages
+    are importable (bioimitation/__init__.py:23-143); returns the IDs."""
+    done = []
+    try:
+        from gym.envs.registration import register
+        for env_id, cls in ENV_CLASSES.items():
+            register(id=env_id, entry_point=f'bioimitation.envs:{cls.__name__}')
+            done.append(env_id)
+    except Exception:
+        pass
+    try:
+        from ray.tune.registry import register_env
+        for env_id, cls in ENV_CLASSES.items():
+            register_env(env_id, lambda config, cls=cls: cls(config))
+    except Exception:
+        pass
+    return done
+
+
+assert set(ENV_CLASSES) <= set(RECIPES)
