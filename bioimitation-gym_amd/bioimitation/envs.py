@@ -10,10 +10,11 @@ torque_walking_imitation_env2D.py:18-366).  Every instance is one env of a
 the HIP kernel, never on the host.  For throughput, step many envs at once
 with ``VectorEnv`` directly.
 
-Reset-index semantics follow the reference exactly: ``random.randint(0, N/2)``
+Reset-index semantics follow the reference exactly: ``random.randint(0, hi)``
 from Python's ``random`` module in train mode (so ``random.seed`` reproduces
-the reference's choice), index 0 in test mode
-(muscle_walking_imitation_env2D.py:133-156).
+the reference's choice) with ``hi = N/2`` (2D envs, Running3D) or ``cycle``
+(Walking3D, LockedKnee3D, Palsy3D), index 0 in test mode
+(muscle_walking_imitation_env2D.py:133-156, muscle_walking_imitation_env3D.py:133-144).
 """
 from __future__ import annotations
 
@@ -98,24 +99,30 @@ class ImitationEnv:
         self.spec = Specification(self.timestep_limit)
         self.spec.action_space = self.action_space
         self.spec.observation_space = self.observation_space
+        self._names = None
 
     # -- reference API -------------------------------------------------------
+    def _out(self, obs, as_dict):
+        o = obs[0].double().cpu().numpy()
+        if not as_dict:
+            return o
+        from .obslayout import load_names, obs_to_dict   # the reference's nested dict, rebuilt host-side
+        if self._names is None:
+            self._names = load_names(self.env_id)
+        return obs_to_dict(o, self._env.pack, self._names)
+
     def reset(self, obs_as_dict=False):
-        if obs_as_dict:
-            raise NotImplementedError('obs_as_dict: the observation is assembled flat on the GPU')
-        index = 0 if self.test else random.randint(0, int(self.N / 2))
+        index = 0 if self.test else random.randint(0, self._env.pack.reset_hi)
         obs = self._env.reset(env_ids=[0], ref_index=[index])
-        return obs[0].double().cpu().numpy()
+        return self._out(obs, obs_as_dict)
 
     def step(self, action, obs_as_dict=False):
-        if obs_as_dict:
-            raise NotImplementedError('obs_as_dict: the observation is assembled flat on the GPU')
         import torch
         a = torch.as_tensor(np.asarray(action, dtype=np.float64).reshape(1, -1), dtype=self._env.dtype,
                             device=self._env.device)
         obs, rew, done, info = self._env.step(a)
         info = info[0].double().cpu().numpy()
-        return [obs[0].double().cpu().numpy(), float(rew[0]), bool(done[0]),
+        return [self._out(obs, obs_as_dict), float(rew[0]), bool(done[0]),
                 {'all_rewards': [float(v) for v in info]}]
 
     def render(self, mode='human', close=False):
@@ -143,7 +150,25 @@ class TorqueWalkingImitationEnv2D(ImitationEnv):
     env_id = 'TorqueWalkingImitation2D-v0'
 
 
-ENV_CLASSES = {c.env_id: c for c in (MuscleWalkingImitationEnv2D, TorqueWalkingImitationEnv2D)}
+class MuscleWalkingImitationEnv3D(ImitationEnv):
+    env_id = 'MuscleWalkingImitation3D-v0'
+
+
+class MuscleRunningImitationEnv3D(ImitationEnv):
+    env_id = 'MuscleRunningImitation3D-v0'
+
+
+class MuscleLockedKneeImitationEnv3D(ImitationEnv):
+    env_id = 'MuscleLockedKneeImitation3D-v0'
+
+
+class MusclePalsyImitationEnv3D(ImitationEnv):
+    env_id = 'MusclePalsyImitation3D-v0'
+
+
+ENV_CLASSES = {c.env_id: c for c in (MuscleWalkingImitationEnv2D, TorqueWalkingImitationEnv2D,
+                                     MuscleWalkingImitationEnv3D, MuscleRunningImitationEnv3D,
+                                     MuscleLockedKneeImitationEnv3D, MusclePalsyImitationEnv3D)}
 
 
 def make(env_id, config=None, **kw):

@@ -165,8 +165,8 @@ class EnvSpec:
     muscle: bool
     three_d: bool
     cycle: int
-    n_episode: int
-    reset_hi: int
+    n_episode: object        # int, or 'rows-2' (N = reference rows - 2)
+    reset_hi: object         # int, or 'N/2'
     w_imitate: float = 0.8
     w_effort: float = 0.2
     w_action: float = 0.1
@@ -455,7 +455,10 @@ def compile_pack(model: OsimModel, spec: EnvSpec, ref: dict) -> P.ModelPack:
     pk.obs_dim = obs_dim_of(model, spec)
     pk.info_dim = 5 if spec.muscle else 4
     pk.nsub, pk.horizon, pk.cycle = spec.nsub, spec.horizon, spec.cycle
-    pk.n_episode, pk.reset_hi = spec.n_episode, spec.reset_hi
+    # 'rows-2': N = q_d.shape[0] - 2; 'N/2': random.randint(0, N/2) (muscle_running_imitation_env3D.py:76,144)
+    nrows_ref = int(ref['time'].shape[0])
+    pk.n_episode = nrows_ref - 2 if spec.n_episode == 'rows-2' else int(spec.n_episode)
+    pk.reset_hi = pk.n_episode // 2 if spec.reset_hi == 'N/2' else int(spec.reset_hi)
     pk.coord_tx = cidx.get('pelvis_tx', -1)
     pk.coord_ty = cidx.get('pelvis_ty', -1)
     pk.coord_tz = cidx.get('pelvis_tz', -1)

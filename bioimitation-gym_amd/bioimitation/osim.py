@@ -47,11 +47,15 @@ def _floats(text) -> np.ndarray:
     return np.array([float(t) for t in (text or '').split()], dtype=np.float64)
 
 
+_FUNCTION_TAGS = ('Constant', 'LinearFunction', 'SimmSpline', 'NaturalCubicSpline', 'MultiplierFunction',
+                  'GCVSpline', 'PiecewiseLinearFunction', 'PolynomialFunction', 'PiecewiseConstantFunction')
+
+
 def _parse_function(elem) -> Function:
     """``elem`` is the element holding one function child (e.g. <function>)."""
     if elem is None:
         return Function('const', b=0.0)
-    kids = [k for k in elem if isinstance(k.tag, str)]
+    kids = [k for k in elem if isinstance(k.tag, str) and k.tag in _FUNCTION_TAGS]
     if not kids:
         return Function('const', b=0.0)
     f = kids[0]
@@ -269,8 +273,11 @@ def _parse_spatial_transform(st, coord_names):
     axes = []
     for ta in st.findall('TransformAxis'):
         cname = (ta.findtext('coordinates') or '').strip() or None
+        fe = ta.find('function')      # 3.x: <function><LinearFunction>…; 4.x: <LinearFunction name="function">
+        if fe is None:
+            fe = ta
         axes.append(TransformAxis(name=ta.get('name'), axis=_vec3(ta.findtext('axis')),
-                                  func=_parse_function(ta.find('function')), coord=cname))
+                                  func=_parse_function(fe), coord=cname))
     return axes
 
 

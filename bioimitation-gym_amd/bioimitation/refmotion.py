@@ -75,25 +75,47 @@ def body_com_table(model, coord_order, q):
     return bodies, out, rot
 
 
-def synthesize_2d_walking(model, ik_mot_path, out_dir, penetration=0.01, dt=0.01):
+def synthesize_reference(model, ik_mot_path, out_dir, coord_map=None, penetration=0.01, dt=0.01):
+    """The AnalyzeTool recipe of ``setup_ka.xml`` (Kinematics + BodyKinematics
+    over the IK ``.mot``, 6 Hz low-pass, ``data/3D/walking_reference_data/setup_ka.xml:72-76``)
+    restated on this package's FK, plus one calibration the recipe does not
+    have: pelvis_ty is shifted so the deepest contact-sphere penetration over
+    the trial is ``penetration`` (the shipped IK puts the feet 2-9 cm into the
+    ground plane of the predictive model), and pelvis_tx starts at 0.
+
+    ``coord_map``: [(model coordinate, IK column, sign)]; None = every model
+    coordinate from the IK column of the same name.  Locked coordinates keep
+    their default value (``Coordinate.setValue`` is a no-op when locked)."""
     header, labels, arr = read_sto(ik_mot_path)
     col = {l: i for i, l in enumerate(labels)}
     t_raw = arr[:, 0]
     coord_order = list(model.coord_order)
+    if coord_map is None:
+        coord_map = [(c, c, 1.0) for c in coord_order]
     q = np.zeros((arr.shape[0], len(coord_order)))
-    for c2d, c3d, sign in SAGITTAL_MAP_2D:
-        v = arr[:, col[c3d]]
-        if c3d not in ('pelvis_tx', 'pelvis_ty', 'pelvis_tz'):
+    for c in coord_order:
+        q[:, coord_order.index(c)] = model.coords[c].default_value
+    for cm, cik, sign in coord_map:
+        if model.coords[cm].locked:
+            continue
+        v = arr[:, col[cik]]
+        if cik not in ('pelvis_tx', 'pelvis_ty', 'pelvis_tz'):
             v = v * math.pi / 180.0
-        q[:, coord_order.index(c2d)] = sign * v
+        q[:, coord_order.index(cm)] = sign * v
     t, q = resample_linear(t_raw, q, dt)
     q = _lowpass(q, dt)
+    for c in coord_order:
+        if model.coords[c].locked:
+            q[:, coord_order.index(c)] = model.coords[c].default_value
     ity = coord_order.index('pelvis_ty')
     lows = np.array([lowest_sphere_y(model, dict(zip(coord_order, row))) for row in q])
     q[:, ity] += -penetration - lows.min()
     itx = coord_order.index('pelvis_tx')
     q[:, itx] -= q[0, itx]
     u = _spline_derivative(t, q)
+    for c in coord_order:
+        if model.coords[c].locked:
+            u[:, coord_order.index(c)] = 0.0
     bodies, com, rot = body_com_table(model, coord_order, q)
     vel = _spline_derivative(t, com)
     os.makedirs(out_dir, exist_ok=True)
@@ -115,6 +137,12 @@ def synthesize_2d_walking(model, ik_mot_path, out_dir, penetration=0.01, dt=0.01
             cols.append(tab[:, -1, a])
         write_sto(os.path.join(out_dir, fname), labs, np.column_stack(cols), name='BodyKinematics')
     return t, q, u
+
+
+def synthesize_2d_walking(model, ik_mot_path, out_dir, penetration=0.01, dt=0.01):
+    """2D walking from the sagittal columns of the 3D IK (the 2D recipe's input
+    ``healthy_gait.sto`` is absent)."""
+    return synthesize_reference(model, ik_mot_path, out_dir, SAGITTAL_MAP_2D, penetration, dt)
 
 
 def load_reference_tables(ref_dir, coord_order, dt=0.01):

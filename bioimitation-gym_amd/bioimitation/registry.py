@@ -33,6 +33,41 @@ RECIPES = {
                   acc_max=1e4, slow_twitch=SLOW_TWITCH_2D)),
 }
 
+# muscle_{walking,running,locked_knee,palsy}_imitation_env3D.py share: done thresholds (limit force 1e4,
+# |qdd| 1e6, calcn_r.z < calcn_l.z; :240-275), reward x (foot_l + foot_r) and exp(-0.5|da|) (:345-351)
+_SPEC_3D = dict(muscle=True, three_d=True, acc_max=1e6, limit_force_max=1e4, action_r_scale=0.5,
+                reward_feet=True, done_cross=True, slow_twitch=SLOW_TWITCH_3D)
+_IK_3D = '3D/inverse_kinematics/task_InverseKinematics.mot'
+_IK_PALSY = '02905/02905_PRE/inverse_kinematics/task_InverseKinematics.mot'
+
+RECIPES.update({
+    # muscle_walking_imitation_env3D.py: cycle 50 (:73), N = rows - 2 (:75), reset randint(0, cycle) (:144)
+    'MuscleWalkingImitation3D-v0': dict(
+        model='3D/scale/model_scaled.osim', transforms=('predictive',),
+        reference='3D/walking_reference_data', ik=_IK_3D,
+        spec=dict(cycle=50, n_episode='rows-2', reset_hi=50, **_SPEC_3D)),
+    # muscle_running_imitation_env3D.py: cycle 70 (:177), N = rows - 2 (:76), reset randint(0, N/2) (:144).
+    # Its running_reference_data/ is absent from the reference (no recipe, no IK): the only shipped 3D
+    # trial (walking) is used, so Running3D differs from Walking3D in cycle/reset range only.
+    'MuscleRunningImitation3D-v0': dict(
+        model='3D/scale/model_scaled.osim', transforms=('predictive',),
+        reference='3D/walking_reference_data', ik=_IK_3D,
+        spec=dict(cycle=70, n_episode='rows-2', reset_hi='N/2', **_SPEC_3D)),
+    # muscle_locked_knee_imitation_env3D.py: prosthetic transform (:104-126), cycle 50 (:75),
+    # N = rows - 2 (:77), reset randint(0, cycle) (:169)
+    'MuscleLockedKneeImitation3D-v0': dict(
+        model='3D/scale/model_scaled.osim', transforms=('predictive', 'prosthetic'),
+        reference='3D/walking_reference_data', ik=_IK_3D,
+        spec=dict(cycle=50, n_episode='rows-2', reset_hi=50, **_SPEC_3D)),
+    # muscle_palsy_imitation_env3D.py: the shipped, already-transformed 02905_PRE model_predictive.osim
+    # (:45, :55-59), physics gets the raw action (:131), cycle 50 (:73), N = rows - 2 (:75), reset
+    # randint(0, cycle) (:144)
+    'MusclePalsyImitation3D-v0': dict(
+        model='02905/02905_PRE/scale/model_predictive.osim', transforms=(),
+        reference='02905/walking_reference_data', ik=_IK_PALSY,
+        spec=dict(cycle=50, n_episode='rows-2', reset_hi=50, raw_action=True, **_SPEC_3D)),
+})
+
 REGISTERED_IDS = [
     'TorqueWalkingImitation2D-v0', 'TorqueRunningImitation2D-v0', 'TorqueJumpingImitation2D-v0',
     'TorqueLockedKneeImitation2D-v0', 'TorqueWalkingImitation3D-v0', 'TorqueRunningImitation3D-v0',
@@ -41,6 +76,26 @@ REGISTERED_IDS = [
     'MuscleLockedKneeImitation2D-v0', 'MuscleWalkingImitation3D-v0', 'MuscleRunningImitation3D-v0',
     'MuscleJumpingImitation3D-v0', 'MuscleLockedKneeImitation3D-v0', 'MusclePalsyImitation3D-v0',
 ]
+
+
+def build_model(env_id: str, ref_data: str, transforms: tuple = None):
+    """The simulated model of ``env_id``: its .osim under the reference's data
+    dir with the recipe's load-time transforms applied (dev container only)."""
+    import os
+    from . import transforms as T
+    from .osim import load_osim
+    r = RECIPES[env_id]
+    m = load_osim(os.path.join(ref_data, r['model']))
+    for t in (r['transforms'] if transforms is None else transforms):
+        if t == 'predictive':
+            m = T.construct_predictive_model(m)
+        elif t == 'torque':
+            m = T.convert_model_to_torque_actuated(m, 200.0)
+        elif t == 'prosthetic':
+            m = T.convert_model_to_prosthetic(m)
+        else:
+            raise ValueError(t)
+    return m
 
 
 def env_spec(env_id: str, config: dict = None) -> EnvSpec:

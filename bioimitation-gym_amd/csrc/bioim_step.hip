@@ -36,6 +36,8 @@
 
 #define DEV __device__ __forceinline__
 #define BIOIM_WG 256 /* threads per workgroup: 256 / G envs share one LDS model image */
+/* env flags baked into a kernel (topologies.h FLAGS); RAW_ACTION, TARGET_OBS, GRF_OBS are run-time */
+#define BIOIM_STRUCT_FLAGS (BIOIM_ENV_MUSCLE | BIOIM_ENV_HAS_TZ | BIOIM_ENV_REWARD_FEET | BIOIM_ENV_DONE_CROSS | BIOIM_ENV_PD)
 
 template <int I, int N, class F>
 DEV void sfor(F &&f) {
@@ -1330,7 +1332,7 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
         for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
             if (hh < H) s += hist[hh];
         curr = s / Real(H);
-        Real phys = (T::FLAGS & BIOIM_ENV_RAW_ACTION) ? a : curr;
+        Real phys = (M.env_flags & BIOIM_ENV_RAW_ACTION) ? a : curr;
         bool pnan = group_any<G>(lane < NA && isnan(phys));
         Real lo = NM > 0 ? Real(0) : SM.ca_min[lane < NA ? lane : 0];
         Real hi = NM > 0 ? Real(1) : SM.ca_max[lane < NA ? lane : 0];
@@ -1816,7 +1818,7 @@ template <class T> bool topology_matches(const bioim_modelpack_t &p) {
     if ((int)unique_curves(p, nullptr).size() != T::NCURVE) return false;
     if (p.nmuscle == 0 && p.nact > SDim<T>::NAD) return false;
     if (p.torso_body != T::TORSO || p.calcn_r_body != T::CALCN_R || p.calcn_l_body != T::CALCN_L) return false;
-    if ((p.env_flags & 0x9fu) != T::FLAGS) return false;
+    if ((p.env_flags & BIOIM_STRUCT_FLAGS) != T::FLAGS) return false;
     for (int c = 0; c < T::NB; ++c) {
         if (p.cbody[c].parent != T::parent[c]) return false;
         uint32_t m = 1u << c;

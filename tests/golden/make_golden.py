@@ -100,6 +100,7 @@ for name, rel in [('bioimitation', 'bioimitation'), ('bioimitation.imitation_env
                   ('bioimitation.imitation_envs.envs', 'bioimitation/imitation_envs/envs'),
                   ('bioimitation.imitation_envs.envs.muscle', 'bioimitation/imitation_envs/envs/muscle'),
                   ('bioimitation.imitation_envs.envs.muscle.planar', 'bioimitation/imitation_envs/envs/muscle/planar'),
+                  ('bioimitation.imitation_envs.envs.muscle.spatial', 'bioimitation/imitation_envs/envs/muscle/spatial'),
                   ('bioimitation.imitation_envs.envs.torque', 'bioimitation/imitation_envs/envs/torque'),
                   ('bioimitation.imitation_envs.envs.torque.planar', 'bioimitation/imitation_envs/envs/torque/planar')]:
     m = types.ModuleType(name)
@@ -322,14 +323,7 @@ oenv.OsimModel = FakeOsimModel
 
 
 def _names(env_id):
-    sys.path.insert(0, os.path.join(REPO, 'bioimitation-gym_amd', 'tools'))
-    osim = sys.modules['bioim_amd.osim']
-    tr = _load_by_path('bioim_amd.transforms', os.path.join(PKG, 'transforms.py'))
-    rec = registry.RECIPES[env_id]
-    m = osim.load_osim(os.path.join(REF, 'bioimitation/imitation_envs/data', rec['model']))
-    for t in rec['transforms']:
-        m = tr.construct_predictive_model(m) if t == 'predictive' else \
-            tr.convert_model_to_torque_actuated(m, 200.0) if t == 'torque' else tr.convert_model_to_prosthetic(m)
+    m = registry.build_model(env_id, os.path.join(REF, 'bioimitation/imitation_envs/data'))
     return dict(coords=list(m.coord_order), bodies=list(m.body_order),
                 muscles=[mu.name for mu in m.muscles] if registry.RECIPES[env_id]['spec']['muscle'] else [],
                 cforces=[h.name for h in m.hc_forces], limits=[l.name for l in m.limits])
@@ -349,7 +343,10 @@ def make_env(env_id, modname, clsname, config):
     mod.construct_predictive_model = lambda *a, **k: None
     if hasattr(mod, 'convert_model_to_torque_actuated'):
         mod.convert_model_to_torque_actuated = lambda *a, **k: None
-    env = getattr(mod, clsname)(config)
+    cls = getattr(mod, clsname)
+    if hasattr(cls, 'convert_model_to_prosthetic'):   # writes the .osim; the pack already holds the result
+        cls.convert_model_to_prosthetic = lambda self, *a, **k: None
+    env = cls(config)
     return env, pk
 
 
@@ -368,6 +365,10 @@ def seed_for_index(target, hi):
 def run_episode(env, pk, seed, T, action_fn, nan_at=()):
     random.seed(seed)
     obs0 = np.array(env.reset(), dtype=np.float64)
+    # the reference's own observation keys, in flatten order (pins bioimitation/obslayout.py)
+    keys = []
+    for k, v in _flatten(env.get_observation_dict()).items():
+        keys.append('.'.join(k) + ('' if isinstance(v, float) else f'#{len(v)}'))
     index = int(round(CURRENT['reset_time'] / 0.01))
     acts, obs, rew, done, info = [], [], [], [], []
     for t in range(T):
@@ -384,7 +385,7 @@ def run_episode(env, pk, seed, T, action_fn, nan_at=()):
         if d:
             break
     return dict(index=index, obs0=obs0, actions=np.array(acts), obs=np.array(obs), reward=np.array(rew),
-                done=np.array(done), info=np.array(info))
+                done=np.array(done), info=np.array(info), obs_keys=np.array(keys))
 
 
 def main():
@@ -434,6 +435,37 @@ def main():
         eps.append(ep)
         print('torque episode', k, 'index', ep['index'], 'steps', len(ep['reward']), 'done', ep['done'][-1])
     out['TorqueWalkingImitation2D-v0'] = eps
+
+    # ---------------- spatial muscle envs (muscle_*_imitation_env3D.py)
+    spatial = [('MuscleWalkingImitation3D-v0', 'muscle_walking_imitation_env3D', 'MuscleWalkingImitationEnv3D'),
+               ('MuscleRunningImitation3D-v0', 'muscle_running_imitation_env3D', 'MuscleRunningImitationEnv3D'),
+               ('MuscleLockedKneeImitation3D-v0', 'muscle_locked_knee_imitation_env3D', 'MuscleLockedKneeImitationEnv3D'),
+               ('MusclePalsyImitation3D-v0', 'muscle_palsy_imitation_env3D', 'MusclePalsyImitationEnv3D')]
+    for j, (env_id, modfile, cls) in enumerate(spatial):
+        mod = 'bioimitation.imitation_envs.envs.muscle.spatial.' + modfile
+        hi = registry.load_pack(env_id).reset_hi
+        eps = []
+        for k, (index, T, nan_at, cfg, lo) in enumerate([(29, 14, (), {}, 0.0), (None, 30, (5,), {}, 0.0),
+                                                         (0, 10, (), {'mode': 'test'}, 0.0),
+                                                         (min(hi, 43), 20, (), {'horizon': 3, 'use_GRF': False}, 0.2)]):
+            config = dict(DEFAULT_CFG, **cfg)
+            env, pk = make_env(env_id, mod, cls, config)
+            seed = 3000 + 10 * j + k if index is None else seed_for_index(index, hi)
+            # a low excitation floor keeps some episodes alive for longer (they fall fast at U[0,1])
+            acts = rng.uniform(lo, 1.0, size=(T, pk.nact)) * (0.3 if k == 3 else 1.0)
+            ep = run_episode(env, pk, seed, T, lambda t, e, acts=acts: acts[t].copy(), nan_at)
+            ep['config'] = repr(config)
+            eps.append(ep)
+            print(env_id, 'episode', k, 'index', ep['index'], 'steps', len(ep['reward']), 'done', ep['done'][-1])
+        config = dict(DEFAULT_CFG)
+        env, pk = make_env(env_id, mod, cls, config)
+        acts = rng.uniform(0.0, 0.5, size=(12, pk.nact))
+        e1 = run_episode(env, pk, seed_for_index(min(hi, 17), hi), 6, lambda t, e: acts[t].copy())
+        e2 = run_episode(env, pk, seed_for_index(min(hi, 18), hi), 6, lambda t, e: acts[6 + t].copy())
+        e1['config'] = e2['config'] = repr(config)
+        e2['chained'] = 1
+        eps += [e1, e2]
+        out[env_id] = eps
 
     for env_id, eps in out.items():
         flat = {}

@@ -12,7 +12,7 @@ def test_make_dispatch_without_gpu():
     with pytest.raises(KeyError):
         envs.make('NoSuchEnv-v0')
     with pytest.raises(NotImplementedError):
-        envs.make('MuscleRunningImitation3D-v0')
+        envs.make('MuscleJumpingImitation3D-v0')
     if not gpu_available():
         with pytest.raises(_lib.BioimError):
             envs.make('MuscleWalkingImitation2D-v0', {'mode': 'test'})
@@ -28,7 +28,8 @@ def test_box_stub():
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not gpu_available(), reason='needs GPU')
-@pytest.mark.parametrize('env_id', ['MuscleWalkingImitation2D-v0', 'TorqueWalkingImitation2D-v0'])
+@pytest.mark.parametrize('env_id', ['MuscleWalkingImitation2D-v0', 'TorqueWalkingImitation2D-v0',
+                                    'MuscleWalkingImitation3D-v0', 'MusclePalsyImitation3D-v0'])
 def test_single_env_matches_oracle(env_id):
     import oracle
     from bioimitation import envs
@@ -41,7 +42,7 @@ def test_single_env_matches_oracle(env_id):
     random.seed(3)
     obs = env.reset()
     random.seed(3)
-    index = random.randint(0, int(pk.n_episode / 2))     # the reference's draw
+    index = random.randint(0, pk.reset_hi)     # the reference's draw (N/2 or cycle)
     ref = orc.reset(bufs, 0, index)
     np.testing.assert_allclose(obs, ref, rtol=1e-9, atol=1e-9)
     assert env.observation_space.shape == (pk.obs_dim,) and env.action_space.shape == (pk.nact,)
@@ -56,4 +57,6 @@ def test_single_env_matches_oracle(env_id):
         assert abs(r - rr) < 1e-7 and d == rd
         assert len(info['all_rewards']) == pk.info_dim
         np.testing.assert_allclose(info['all_rewards'], rinfo, rtol=1e-7, atol=1e-7)
+    d = env.step(env.action_space.sample(rng), obs_as_dict=True)[0]      # the reference's nested dict
+    assert set(d) >= {'phase', 'coordinate_pos', 'coordinate_vel', 'body_pos'} and len(d['body_pos']) == 10
     env.close()

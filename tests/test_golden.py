@@ -10,8 +10,9 @@ import pytest
 
 from bioimitation.registry import load_pack
 
-GOLDEN = {'MuscleWalkingImitation2D-v0': 'tests/golden/MuscleWalkingImitation2D-v0.npz',
-          'TorqueWalkingImitation2D-v0': 'tests/golden/TorqueWalkingImitation2D-v0.npz'}
+GOLDEN = {e: f'tests/golden/{e}.npz' for e in (
+    'MuscleWalkingImitation2D-v0', 'TorqueWalkingImitation2D-v0', 'MuscleWalkingImitation3D-v0',
+    'MuscleRunningImitation3D-v0', 'MuscleLockedKneeImitation3D-v0', 'MusclePalsyImitation3D-v0')}
 
 
 def episodes(path):
@@ -40,3 +41,28 @@ def test_oracle_matches_reference_env_semantics(env_id, oracle_lib):
             assert abs(r - ep['reward'][t]) < 1e-11, (t, r, ep['reward'][t])
             assert d == bool(ep['done'][t])
             np.testing.assert_allclose(info, ep['info'][t], rtol=1e-11, atol=1e-12)
+
+
+@pytest.mark.parametrize('env_id', list(GOLDEN))
+def test_obs_layout_matches_reference_keys(env_id):
+    """bioimitation/obslayout.py labels every flat column exactly as the
+    reference's flatten(get_observation_dict()) orders its keys, for every
+    config the fixtures cover (target obs / GRF switches, horizon)."""
+    import os
+    from bioimitation.obslayout import column_names, load_names, obs_to_dict
+    path = os.path.join(os.path.dirname(os.path.dirname(__file__)), GOLDEN[env_id])
+    names = load_names(env_id)
+    for ep in episodes(path):
+        cfg = ast.literal_eval(str(ep['config']))
+        pk = load_pack(env_id, cfg)
+        ref_cols = []
+        for k in ep['obs_keys']:
+            k = str(k)
+            if '#' in k:
+                base, n = k.split('#')
+                ref_cols += [f'{base}[{i}]' for i in range(int(n))]
+            else:
+                ref_cols.append(k)
+        assert column_names(pk, names) == ref_cols
+        d = obs_to_dict(ep['obs0'], pk, names)
+        assert d['phase'] == ep['obs0'][0] and len(d['coordinate_vel']) == pk.ncoord

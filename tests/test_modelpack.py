@@ -41,6 +41,28 @@ def test_model_facts(env_id, obs, act, info):
     assert quirks[:7] == [29, 58, 59, 116, 117, 118, 119] and len(quirks) == 16
 
 
+# SURVEY.md 8.0 (3D rows): coords (free), composite bodies, muscles, obs; masses from the .osim files
+@pytest.mark.parametrize('env_id,ndof,ncbody,nm,obs,mass,cycle,n_episode,reset_hi', [
+    ('MuscleWalkingImitation3D-v0', 14, 7, 22, 201, 41.5, 50, 362, 50),
+    ('MuscleRunningImitation3D-v0', 14, 7, 22, 201, 41.5, 70, 362, 181),
+    ('MuscleLockedKneeImitation3D-v0', 12, 5, 19, 192, 41.5, 50, 362, 50),
+    ('MusclePalsyImitation3D-v0', 14, 7, 22, 201, 35.0, 50, 476, 50)])
+def test_model_facts_3d(env_id, ndof, ncbody, nm, obs, mass, cycle, n_episode, reset_hi):
+    pk = load_pack(env_id)
+    assert pk.ncoord == 17 and pk.nosbody == 13
+    assert (pk.ndof, pk.ncbody, pk.nmuscle, pk.nact, pk.obs_dim, pk.info_dim) == (ndof, ncbody, nm, nm, obs, 5)
+    assert abs(pk.total_mass - mass) < 1e-9
+    assert (pk.cycle, pk.n_episode, pk.reset_hi) == (cycle, n_episode, reset_hi)
+    assert pk.nsphere == 6 and pk.ncforce == 2 and pk.nlimit == 6
+    assert pk.env_flags & (P.ENV_HAS_TZ | P.ENV_REWARD_FEET | P.ENV_DONE_CROSS) == \
+        P.ENV_HAS_TZ | P.ENV_REWARD_FEET | P.ENV_DONE_CROSS
+    assert bool(pk.env_flags & P.ENV_RAW_ACTION) == (env_id == 'MusclePalsyImitation3D-v0')
+    assert (pk.acc_max, pk.limit_force_max, pk.action_r_scale) == (1e6, 1e4, 0.5)
+    # locked: hip_rotation_r/l, lumbar_extension (+ knee_angle_l, ankle_angle_l for the prosthetic)
+    locked = [c for c in range(pk.ncoord) if pk.coord[c].dof < 0]
+    assert locked == ([8, 13, 16] if ndof == 14 else [8, 13, 14, 15, 16])
+
+
 def test_config_patching():
     base = load_pack('MuscleWalkingImitation2D-v0')
     pk = load_pack('MuscleWalkingImitation2D-v0', {'use_target_obs': False, 'use_GRF': False, 'horizon': 3,
@@ -93,13 +115,12 @@ def test_predictive_transform_known_answer():
 @pytest.mark.skipif(not os.path.isdir(REF_DATA), reason='reference data not present')
 def test_committed_packs_are_current():
     """The committed packs equal a fresh compile from the reference data."""
-    import sys
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), 'bioimitation-gym_amd', 'tools'))
-    import build_packs
     from bioimitation import modelpack, refmotion, registry
+    data = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'bioimitation-gym_amd',
+                        'bioimitation', 'data')
     for env_id, rec in registry.RECIPES.items():
-        model = build_packs.load_model(REF_DATA, rec)
-        ref = refmotion.load_reference_tables(os.path.join(build_packs.DATA, rec['reference']), model.coord_order)
+        model = registry.build_model(env_id, REF_DATA)
+        ref = refmotion.load_reference_tables(os.path.join(data, rec['reference']), model.coord_order)
         fresh = modelpack.pack_bytes(modelpack.compile_pack(model, registry.env_spec(env_id), ref))
         committed = modelpack.pack_bytes(load_pack(env_id))
         assert fresh == committed, env_id

@@ -1,62 +1,93 @@
 """Physics invariants of the fp64 oracle (parity with OpenSim itself is
 unpinned — OpenSim is not available — so the restatement is checked against
-mechanics identities instead)."""
+mechanics identities instead).  Every invariant runs on
+the planar model and on the spatial models (3D rotations, locked coordinates,
+the prosthetic topology, the shipped palsy model)."""
+import os
+
 import numpy as np
 import pytest
 
 from bioimitation.registry import load_pack
 
-ENV = 'MuscleWalkingImitation2D-v0'
+ENVS = ['MuscleWalkingImitation2D-v0', 'MuscleRunningImitation3D-v0', 'MuscleLockedKneeImitation3D-v0',
+        'MusclePalsyImitation3D-v0']
+REF_DATA = '/root/reference/bioimitation/imitation_envs/data'
 
 
-@pytest.fixture(scope='module')
-def orc(oracle_lib):
-    return oracle_lib.Oracle(load_pack(ENV))
+@pytest.fixture(scope='module', params=ENVS)
+def orc(request, oracle_lib):
+    return oracle_lib.Oracle(load_pack(request.param))
+
+
+def dof_of(pk, name_index):
+    return pk.coord[name_index].dof
+
+
+def ref_dofs(pk, row):
+    """reference row r as a dof vector (locked coordinates dropped)"""
+    q = np.zeros(pk.ndof)
+    u = np.zeros(pk.ndof)
+    for c in range(pk.ncoord):
+        d = pk.coord[c].dof
+        if d >= 0:
+            q[d], u[d] = pk.ref_q[row][c], pk.ref_u[row][c]
+    return q, u
+
+
+def random_q(pk, rng, scale=0.5):
+    """random pose around reference row 40"""
+    q, _ = ref_dofs(pk, 40)
+    return q + rng.normal(0, scale, pk.ndof)
 
 
 def test_forward_kinematics_matches_raw_joint_chain(orc):
     """Composite-body FK (compiled pack) == FK straight from the parsed joints."""
-    import os
-    from bioimitation import modelpack, transforms
-    from bioimitation.osim import load_osim
-    path = '/root/reference/bioimitation/imitation_envs/data/2D/scale/model_scaled.osim'
-    if not os.path.exists(path):
+    from bioimitation import modelpack, registry
+    if not os.path.isdir(REF_DATA):
         pytest.skip('reference data not present')
-    m = transforms.construct_predictive_model(load_osim(path))
+    pk = orc.pack
+    m = registry.build_model(pk.env_id.decode(), REF_DATA)
     rng = np.random.default_rng(0)
     for _ in range(5):
-        q = rng.normal(0, 0.5, 9)
+        q = random_q(pk, rng)
         R, p, com = orc.fk(q)
-        poses, com2 = modelpack.raw_forward_kinematics(m, dict(zip(m.coord_order, q)))
+        qv = {c: q[pk.coord[i].dof] for i, c in enumerate(m.coord_order) if pk.coord[i].dof >= 0}
+        poses, com2 = modelpack.raw_forward_kinematics(m, qv)
         for i, b in enumerate(m.body_order):
-            np.testing.assert_allclose(p[i], poses[b][1], atol=1e-14)
-            np.testing.assert_allclose(R[i], poses[b][0], atol=1e-14)
-        np.testing.assert_allclose(com, com2, atol=1e-14)
+            np.testing.assert_allclose(p[i], poses[b][1], atol=1e-13)
+            np.testing.assert_allclose(R[i], poses[b][0], atol=1e-13)
+        np.testing.assert_allclose(com, com2, atol=1e-13)
 
 
 def test_mass_matrix_spd_and_translational_mass(orc):
+    pk = orc.pack
     rng = np.random.default_rng(1)
+    trans = [pk.coord[c].dof for c in (pk.coord_tx, pk.coord_ty, pk.coord_tz) if c >= 0]
     for _ in range(5):
-        M, _ = orc.mass_bias(rng.normal(0, 0.5, 9), rng.normal(0, 1, 9))
+        M, _ = orc.mass_bias(random_q(pk, rng), rng.normal(0, 1, pk.ndof))
         assert np.abs(M - M.T).max() == 0.0
         assert np.linalg.eigvalsh(M).min() > 0
-        assert abs(M[1, 1] - 75.1646) < 1e-9 and abs(M[2, 2] - 75.1646) < 1e-9
+        for d in trans:      # pelvis translations are along ground axes: the whole mass
+            assert abs(M[d, d] - pk.total_mass) < 1e-9
 
 
-def test_bias_equals_lagrangian_coriolis(oracle_lib):
+@pytest.mark.parametrize('env_id', ENVS)
+def test_bias_equals_lagrangian_coriolis(oracle_lib, env_id):
     """bias(q,u) with g=0 equals Mdot u - 1/2 d(u'Mu)/dq (finite differences)."""
-    pk = load_pack(ENV)
+    pk = load_pack(env_id)
     pk.gravity[1] = 0.0
     o = oracle_lib.Oracle(pk)
     rng = np.random.default_rng(2)
     h = 1e-6
+    nd = pk.ndof
     for _ in range(3):
-        q, u = rng.normal(0, 0.5, 9), rng.normal(0, 2, 9)
+        q, u = random_q(pk, rng), rng.normal(0, 2, nd)
         M, b = o.mass_bias(q, u)
         Md = np.zeros_like(M)
-        grad = np.zeros(9)
-        for k in range(9):
-            e = np.zeros(9); e[k] = h
+        grad = np.zeros(nd)
+        for k in range(nd):
+            e = np.zeros(nd); e[k] = h
             Mp, _ = o.mass_bias(q + e, u)
             Mm, _ = o.mass_bias(q - e, u)
             Md += (Mp - Mm) / (2 * h) * u[k]
@@ -66,31 +97,38 @@ def test_bias_equals_lagrangian_coriolis(oracle_lib):
 
 def test_gravity_bias_is_potential_gradient(orc):
     pk = orc.pack
-    q = np.random.default_rng(3).normal(0, 0.5, 9)
-    _, b = orc.mass_bias(q, np.zeros(9))
+    nd = pk.ndof
+    q = random_q(pk, np.random.default_rng(3))
+    _, b = orc.mass_bias(q, np.zeros(nd))
     g = np.array(pk.gravity[:])
 
     def V(qq):
         return -pk.total_mass * g @ orc.fk(qq)[2]
     h = 1e-6
-    grad = np.array([(V(q + h * np.eye(9)[k]) - V(q - h * np.eye(9)[k])) / (2 * h) for k in range(9)])
+    grad = np.array([(V(q + h * np.eye(nd)[k]) - V(q - h * np.eye(nd)[k])) / (2 * h) for k in range(nd)])
     np.testing.assert_allclose(b, grad, atol=1e-6)
 
 
 def test_moment_arms_are_path_length_gradients(orc):
     pk = orc.pack
-    q, u = np.array(pk.ref_q[50][:9]), np.array(pk.ref_u[50][:9])
+    nd = pk.ndof
+    q, u = ref_dofs(pk, 50)
     h = 1e-7
     for m in range(pk.nmuscle):
         L, Ld, d = orc.muscle_path(q, u, m)
-        fd = np.array([(orc.muscle_path(q + h * np.eye(9)[k], u, m)[0] -
-                        orc.muscle_path(q - h * np.eye(9)[k], u, m)[0]) / (2 * h) for k in range(9)])
+        fd = np.array([(orc.muscle_path(q + h * np.eye(nd)[k], u, m)[0] -
+                        orc.muscle_path(q - h * np.eye(nd)[k], u, m)[0]) / (2 * h) for k in range(nd)])
         np.testing.assert_allclose(d, fd, atol=1e-8)
         assert abs(Ld - d @ u) < 1e-12
 
 
 def test_millard_curve_landmarks(orc):
     # ActiveForceLength peak, ForceVelocity isometric/vmax, passive and tendon toe
+    # (4.1 default curve parameters; the palsy model sets fal minimum_value=0, 02905_PRE
+    # model_predictive.osim:1855, so its plateau landmark differs)
+    palsy = orc.pack.env_id.decode() == 'MusclePalsyImitation3D-v0'
+    if palsy:
+        pytest.skip('explicit curve parameters (checked by the curve tests)')
     assert abs(orc.curve(0, 0, 1.0)[0] - 1.0) < 1e-12
     assert abs(orc.curve(0, 0, 0.3)[0] - 0.1) < 1e-12          # minimum_value plateau
     y, d = orc.curve(0, 1, 0.0)
@@ -117,28 +155,34 @@ def test_static_equilibrium_balances_fiber_and_tendon(orc):
 
 def test_contact_pushes_up_and_opposes_slip(orc):
     pk = orc.pack
-    q = np.array(pk.ref_q[0][:9])
-    q[2] -= 0.02                   # sink 2 cm into the ground
-    u = np.zeros(9)
-    u[1] = 0.5                     # pelvis sliding forward
+    q, _ = ref_dofs(pk, 0)
+    dx, dy = pk.coord[pk.coord_tx].dof, pk.coord[pk.coord_ty].dof
+    q[dy] -= 0.02                  # sink 2 cm into the ground
+    u = np.zeros(pk.ndof)
+    u[dx] = 0.5                    # pelvis sliding forward
     tau, w = orc.contact(q, u)
     Fy = w[1] + w[7]
     Fx = w[0] + w[6]
     assert Fy > 0 and Fx < 0
-    assert abs(tau[2] - Fy) < 1e-9 and abs(tau[1] - Fx) < 1e-9   # translational dofs see the net force
+    # translational dofs see the net force
+    assert abs(tau[dy] - Fy) < 1e-9 * Fy and abs(tau[dx] - Fx) < 1e-9 * Fy
+    if pk.coord_tz >= 0:
+        assert abs(tau[pk.coord[pk.coord_tz].dof] - (w[2] + w[8])) < 1e-9 * Fy
 
 
-def test_energy_conserved_without_dissipation(oracle_lib):
-    """Torque model, zero controls, gravity only (no contact: model lifted),
-    small substeps: total energy drifts only at O(dt)."""
-    pk = load_pack('TorqueWalkingImitation2D-v0', {'nsub': 200})
+@pytest.mark.parametrize('env_id', ['TorqueWalkingImitation2D-v0', 'MuscleRunningImitation3D-v0'])
+def test_energy_conserved_without_dissipation(oracle_lib, env_id):
+    """Zero controls (muscles removed), gravity only (no contact: model
+    lifted), small substeps: total energy drifts only at O(dt)."""
+    pk = load_pack(env_id, {'nsub': 200})
     pk.nlimit = 0
+    pk.nmuscle = 0
     o = oracle_lib.Oracle(pk)
     envs = o.new_envs(1)
     o.reset(envs, 0, 10)
     s = o.get_state(envs, 0)
     nd = pk.ndof
-    s[5 + 2] += 1.0                # lift the pelvis 1 m: no contact during the test
+    s[5 + pk.coord[pk.coord_ty].dof] += 1.0   # lift the pelvis 1 m: no contact during the test
     s[5 + nd:5 + 2 * nd] = np.random.default_rng(4).normal(0, 0.5, nd)
     o.set_state(envs, 0, s)
 
