@@ -68,6 +68,9 @@ def main():
     ap.add_argument('--precision', type=int, default=int(os.environ.get('BIOIM_PRECISION', 64)))
     ap.add_argument('--env-id', default='MuscleWalkingImitation2D-v0')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--mixed', default=None,
+                    help="mixed batch 'ID_A,ID_B' split 50/50 per GPU (BASELINE config C5), e.g. "
+                         "MuscleLockedKneeImitation3D-v0,MusclePalsyImitation3D-v0")
     a = ap.parse_args()
 
     import numpy as np
@@ -82,9 +85,20 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
 
-    from bioimitation.vector_env import VectorEnv
-    env = VectorEnv(a.env_id, a.envs, device=local, precision=a.precision, seed=1000, auto_reset=True,
-                    env_offset=rank * a.envs)        # global env index block (bioimitation/parallel.py)
+    from bioimitation.vector_env import MixedVectorEnv, VectorEnv
+    if a.mixed:
+        ids = a.mixed.split(',')
+        sizes = [a.envs // len(ids)] * len(ids)
+        sizes[-1] += a.envs - sum(sizes)
+        env = MixedVectorEnv(list(zip(ids, sizes)), device=local, precision=a.precision, seed=1000, auto_reset=True,
+                             env_offset=rank * a.envs)
+        env.pack, env.nsub, env.lanes_per_env = env.envs[0].pack, env.envs[0].nsub, env.envs[0].lanes_per_env
+        env.launch = {e.env_id: e.launch for e in env.envs}
+        a.env_id = '+'.join(ids)
+        a.no_cpu_baseline = True
+    else:
+        env = VectorEnv(a.env_id, a.envs, device=local, precision=a.precision, seed=1000, auto_reset=True,
+                        env_offset=rank * a.envs)        # global env index block (bioimitation/parallel.py)
     n, A = a.envs, env.action_dim
     total = a.warmup + a.steps
     gen = np.random.Generator(np.random.PCG64(rank))
@@ -117,9 +131,11 @@ def main():
     steps_total = world * n * a.steps
     value = steps_total / t_max
     if rank == 0:
-        pk = env.pack
         real_bytes = 8 if a.precision == 64 else 4
-        B = algorithmic_bytes_per_env_step(pk, real_bytes)
+        if a.mixed:   # env-weighted mean over the segments
+            B = sum(algorithmic_bytes_per_env_step(e.pack, real_bytes) * e.num_envs for e in env.envs) / n
+        else:
+            B = algorithmic_bytes_per_env_step(env.pack, real_bytes)
         achieved = B * n / (kernel_ms * 1e-3) / 1e9
         traffic = None
         tf = os.path.join(REPO, 'profiles', 'traffic.json')
@@ -137,7 +153,8 @@ def main():
             'vs_baseline': None, 'dtype': f'f{a.precision}',
             'data': 'synthetic: PCG64 U[0,1] muscle excitations; reference motion synthesized from the shipped 3D IK',
             'config': {'workload': f'{a.env_id} batched env.step, {n} envs/GPU, nsub={env.nsub}, auto-reset',
-                       'envs_per_gpu': n, 'lanes_per_env': env.lanes_per_env, 'parallelism': f'env-shard x{world}'},
+                       'envs_per_gpu': n, 'lanes_per_env': env.lanes_per_env, 'parallelism': f'env-shard x{world}',
+                       'launch': env.launch},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                          'bytes_per_env_step': B, 'kernel_ms': kernel_ms},

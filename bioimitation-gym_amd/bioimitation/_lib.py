@@ -15,8 +15,8 @@ from . import packdef as P
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get('BIOIM_LIB', os.path.join(PKG_ROOT, 'build', 'libbioim.so'))
 
-EXPORTS = ['bioim_create', 'bioim_destroy', 'bioim_reset', 'bioim_step', 'bioim_set_auto_reset', 'bioim_set_env_offset', 'bioim_state_dim',
-           'bioim_get_state', 'bioim_set_state', 'bioim_query', 'bioim_stream', 'bioim_set_stream', 'bioim_sync',
+EXPORTS = ['bioim_create', 'bioim_destroy', 'bioim_reset', 'bioim_step', 'bioim_set_auto_reset', 'bioim_set_env_offset', 'bioim_set_io_strides', 'bioim_step_group', 'bioim_state_dim',
+           'bioim_get_state', 'bioim_set_state', 'bioim_query', 'bioim_query_launch', 'bioim_stream', 'bioim_set_stream', 'bioim_sync',
            'bioim_last_error', 'bioim_modelpack_size']
 
 _lib = None
@@ -41,10 +41,13 @@ def load():
         'bioim_step': (C.c_int, [vp, vp, vp, vp, vp, vp]),
         'bioim_set_auto_reset': (C.c_int, [vp, C.c_int]),
         'bioim_set_env_offset': (C.c_int, [vp, C.c_int]),
+        'bioim_set_io_strides': (C.c_int, [vp, C.c_int, C.c_int, C.c_int]),
+        'bioim_step_group': (C.c_int, [C.POINTER(vp), C.c_int, vp, vp, vp, vp, vp]),
         'bioim_state_dim': (C.c_int, [vp]),
         'bioim_get_state': (C.c_int, [vp, dp]),
         'bioim_set_state': (C.c_int, [vp, dp]),
         'bioim_query': (C.c_int, [vp, i32p]),
+        'bioim_query_launch': (C.c_int, [vp, i32p]),
         'bioim_stream': (vp, [vp]),
         'bioim_set_stream': (C.c_int, [vp, vp]),
         'bioim_sync': (C.c_int, [vp]),

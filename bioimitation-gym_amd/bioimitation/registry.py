@@ -68,6 +68,10 @@ RECIPES.update({
         spec=dict(cycle=50, n_episode='rows-2', reset_hi=50, raw_action=True, **_SPEC_3D)),
 })
 
+# mixed-topology batches (BASELINE.json config C5, bench.py --mixed): the prosthetic (12 dof,
+# 19 muscles) next to the palsy model (14 dof, 22 muscles)
+MIXED_BATCHES = [('MuscleLockedKneeImitation3D-v0', 'MusclePalsyImitation3D-v0')]
+
 REGISTERED_IDS = [
     'TorqueWalkingImitation2D-v0', 'TorqueRunningImitation2D-v0', 'TorqueJumpingImitation2D-v0',
     'TorqueLockedKneeImitation2D-v0', 'TorqueWalkingImitation3D-v0', 'TorqueRunningImitation3D-v0',

@@ -40,6 +40,10 @@ class VectorEnv:
         _lib.check(L.bioim_query(h, q))
         self.obs_dim, self.action_dim, self.info_dim, self.lanes_per_env, self.nsub, self.state_dim = \
             q[1], q[2], q[3], q[5], q[6], q[7]
+        ql = (C.c_int32 * 5)()
+        _lib.check(L.bioim_query_launch(h, ql))
+        self.launch = dict(lanes_per_env=ql[0], threads_per_workgroup=ql[1], envs_per_workgroup=ql[2],
+                           lds_bytes_per_workgroup=ql[3], workgroups=ql[4])
         _lib.check(L.bioim_set_auto_reset(h, 1 if auto_reset else 0))
         _lib.check(L.bioim_set_env_offset(h, int(env_offset)))
         self.env_offset = int(env_offset)
@@ -106,3 +110,68 @@ class VectorEnv:
             self.close()
         except Exception:
             pass
+
+
+class MixedVectorEnv:
+    """A batch of several env IDs on one GPU (BASELINE.json config C5:
+    MuscleLockedKneeImitation3D-v0 + MusclePalsyImitation3D-v0), stepped by
+    ``bioim_step_group``: segment i owns rows [off_i, off_i + n_i) of padded
+    buffers — actions (N, max A), obs (N, max O), info (N, max I) — with
+    ``action_mask`` / ``obs_mask`` marking each row's valid columns; one
+    launch per segment, in order, on the first segment's stream.
+    Device-drawn reset rows are keyed by the global env index (``env_offset``
+    + row), as in :class:`VectorEnv`, so the batch reproduces each segment
+    stepped alone bit for bit."""
+
+    def __init__(self, segments, config=None, device: int = 0, precision: int = 64, seed: int = 0,
+                 auto_reset: bool = False, env_offset: int = 0):
+        import torch
+        self.envs, off = [], 0
+        for env_id, n in segments:
+            self.envs.append(VectorEnv(env_id, n, config=config, device=device, precision=precision, seed=seed,
+                                       auto_reset=auto_reset, env_offset=env_offset + off))
+            off += int(n)
+        self.num_envs = off
+        self.device, self.dtype, self.precision = self.envs[0].device, self.envs[0].dtype, precision
+        self.action_dim = max(e.action_dim for e in self.envs)
+        self.obs_dim = max(e.obs_dim for e in self.envs)
+        self.info_dim = max(e.info_dim for e in self.envs)
+        n, dev = self.num_envs, self.device
+        self.obs = torch.zeros((n, self.obs_dim), dtype=self.dtype, device=dev)
+        self.reward = torch.zeros(n, dtype=self.dtype, device=dev)
+        self.done = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.info = torch.zeros((n, self.info_dim), dtype=self.dtype, device=dev)
+        self.action_mask = torch.zeros((n, self.action_dim), dtype=torch.bool, device=dev)
+        self.obs_mask = torch.zeros((n, self.obs_dim), dtype=torch.bool, device=dev)
+        self.offsets = []
+        off = 0
+        for e in self.envs:
+            _lib.check(e._L.bioim_set_io_strides(e._h, self.action_dim, self.obs_dim, self.info_dim))
+            sl = slice(off, off + e.num_envs)
+            e.obs, e.reward, e.done, e.info = self.obs[sl], self.reward[sl], self.done[sl], self.info[sl]
+            self.action_mask[sl, :e.action_dim] = True
+            self.obs_mask[sl, :e.obs_dim] = True
+            self.offsets.append(off)
+            off += e.num_envs
+        self._hs = (C.c_void_p * len(self.envs))(*[e._h.value for e in self.envs])
+        self._L = self.envs[0]._L
+
+    def reset(self):
+        for e in self.envs:
+            e.reset()
+        return self.obs
+
+    def step(self, actions):
+        """actions: (N, max A) tensor; columns beyond a row's own action dim are ignored."""
+        a = actions
+        if a.dtype != self.dtype or a.device != self.device or not a.is_contiguous():
+            a = a.to(device=self.device, dtype=self.dtype).contiguous()
+        assert a.shape == (self.num_envs, self.action_dim), a.shape
+        p = VectorEnv._ptr
+        _lib.check(self._L.bioim_step_group(self._hs, len(self.envs), p(a), p(self.obs), p(self.reward),
+                                            p(self.done), p(self.info)))
+        return self.obs, self.reward, self.done, self.info
+
+    def close(self):
+        for e in self.envs:
+            e.close()

@@ -1230,25 +1230,42 @@ DEV int draw_index(uint64_t seed, int env, int count, int hi) {
 }
 
 /* ---------------------------------------------------------------- kernel
- * One 64-lane workgroup = 64/G envs.  mode 0: env step (optionally with
- * in-kernel auto-reset); mode 1: reset the listed envs. */
+ * Launch arguments of one env segment (one handle).  mode 0: env step
+ * (optionally with in-kernel auto-reset); mode 1: reset the listed envs.
+ * I/O rows are strided so several segments (a mixed-topology group) can
+ * share padded [N_total][stride] buffers. */
+template <class T, typename Real> struct LaunchArgs {
+    const DModel<Real> *Mg;
+    const SModel<T, Real> *Sg;
+    DState<Real> st;
+    int N, mode, n_list, auto_reset, env_offset, blocks;
+    int act_stride, obs_stride, info_stride;
+    const Real *actions;
+    Real *obs, *reward, *info;
+    uint8_t *done_out;
+    const int32_t *env_ids, *ref_index;
+    uint64_t seed;
+};
+
+/* One 256-thread workgroup = 256/G envs of segment `a`, block `blk`. */
 template <class T, typename Real>
-__global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))) void env_kernel(
-    const DModel<Real> *__restrict__ Mg, const SModel<T, Real> *__restrict__ Sg, DState<Real> st, int N, int mode,
-    const Real *__restrict__ actions, Real *__restrict__ obs, Real *__restrict__ reward, uint8_t *__restrict__ done_out,
-    Real *__restrict__ info, const int32_t *__restrict__ env_ids, const int32_t *__restrict__ ref_index, int n_list,
-    int auto_reset, uint64_t seed, int env_offset) {
+DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     using LY = Lay<T, Real>;
     constexpr int G = T::G, ND = LY::ND, NA = T::NA, NM = T::NM;
     constexpr int EPB = BIOIM_WG / G;
     constexpr size_t SMB = smodel_bytes<T, Real>();
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const DModel<Real> *__restrict__ Mg = a.Mg;
+    const DState<Real> &st = a.st;
+    const int N = a.N, mode = a.mode;
+    const Real *__restrict__ actions = a.actions;
+    Real *__restrict__ obs = a.obs;
 #ifdef BIOIM_STAMPS
     const unsigned long long k_t0 = __builtin_amdgcn_s_memtime();
 #endif
     /* stage the shared model image (one copy per workgroup) */
     {
-        const uint4 *src = reinterpret_cast<const uint4 *>(Sg);
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.Sg);
         uint4 *dst = reinterpret_cast<uint4 *>(smem_raw);
         for (int i = threadIdx.x; i < (int)(SMB / 16); i += BIOIM_WG) dst[i] = src[i];
     }
@@ -1261,12 +1278,12 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
     const DModel<Real> &M = *Mg;
     const int lane = threadIdx.x % G;
     const int slot = threadIdx.x / G;
-    int gidx = blockIdx.x * EPB + slot;
+    int gidx = blk * EPB + slot;
     Real *lds = reinterpret_cast<Real *>(smem_raw + SMB) + slot * LY::SIZE;
     int env;
     if (mode == 1) {
-        if (gidx >= n_list) return;
-        env = env_ids ? env_ids[gidx] : gidx;
+        if (gidx >= a.n_list) return;
+        env = a.env_ids ? a.env_ids[gidx] : gidx;
         if (env < 0 || env >= N) return;
     } else {
         if (gidx >= N) return;
@@ -1293,13 +1310,13 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
     Real rew = 0, inf[5] = {0, 0, 0, 0, 0};
     bool do_reset = (mode == 1);
     int reset_row = 0;
-    if (mode == 1) reset_row = ref_index ? ref_index[gidx] : draw_index(seed, env_offset + env, resets, M.reset_hi);
+    if (mode == 1) reset_row = a.ref_index ? a.ref_index[gidx] : draw_index(a.seed, a.env_offset + env, resets, M.reset_hi);
 
     int remaining = 0;
     Real dt = 0;
     if (mode == 0) {
         /* ---- action pre-processing (Env.step) */
-        Real raw = lane < NA ? actions[(size_t)env * NA + lane] : Real(0);
+        Real raw = lane < NA ? actions[(size_t)env * a.act_stride + lane] : Real(0);
         bool anynan = group_any<G>(lane < NA && isnan(raw));
         Real a = anynan ? Real(0) : raw;
         if constexpr ((T::FLAGS & BIOIM_ENV_PD) != 0) {
@@ -1467,7 +1484,7 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
         }
         wave_sync();
         if (obs)
-            for (int k = lane; k < M.obs_dim; k += G) obs[(size_t)env * M.obs_dim + k] = ob[k];
+            for (int k = lane; k < M.obs_dim; k += G) obs[(size_t)env * a.obs_stride + k] = ob[k];
         wave_sync();
         if (reported_reset) break;
 
@@ -1560,20 +1577,20 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
             done = d_;
         }
         if (lane == 0) {
-            if (reward) reward[env] = rew;
-            done_out[env] = (uint8_t)done;
+            if (a.reward) a.reward[env] = rew;
+            a.done_out[env] = (uint8_t)done;
         }
-        if (info && lane < M.info_dim) {
+        if (a.info && lane < M.info_dim) {
             Real iv = inf[0];
 #pragma unroll
             for (int i = 1; i < 5; ++i) iv = lane == i ? inf[i] : iv;
-            info[(size_t)env * M.info_dim + lane] = iv;
+            a.info[(size_t)env * a.info_stride + lane] = iv;
         }
         wave_sync();
-        if (done && auto_reset) {
+        if (done && a.auto_reset) {
             pending_reset = true;
             do_reset = true;
-            reset_row = draw_index(seed, env_offset + env, resets, M.reset_hi);
+            reset_row = draw_index(a.seed, a.env_offset + env, resets, M.reset_hi);
             continue;
         }
         break;
@@ -1606,6 +1623,12 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
             if (hh < H) st.hist[((size_t)hh * NA + lane) * N + env] = hist[hh];
     }
 }
+
+template <class T, typename Real>
+__global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))) void env_kernel(LaunchArgs<T, Real> a) {
+    env_block<T, Real>(a, blockIdx.x);
+}
+
 
 /* =================================================================== host */
 namespace {
@@ -1866,6 +1889,7 @@ struct Ops {
 
 struct bioim_handle {
     int n, device, precision, ndof, nmuscle, nact, horizon, obs_dim, info_dim, nsub, auto_reset, env_offset;
+    int act_stride, obs_stride, info_stride; /* I/O row strides (default nact, obs_dim, info_dim) */
     uint64_t seed;
     hipStream_t stream;
     bool own_stream;
@@ -1885,20 +1909,34 @@ template <class T, typename Real> constexpr size_t lds_bytes() {
 }
 
 template <class T, typename Real>
+LaunchArgs<T, Real> make_args(bioim_handle_t *h, int mode, const void *actions, void *obs, void *reward, uint8_t *done,
+                              void *info, const int32_t *env_ids, const int32_t *ref_index, int n_list) {
+    constexpr int EPB = BIOIM_WG / T::G;
+    LaunchArgs<T, Real> a;
+    const int count = mode == 1 ? n_list : h->n;
+    a.Mg = reinterpret_cast<const DModel<Real> *>(h->model);
+    a.Sg = reinterpret_cast<const SModel<T, Real> *>(h->smodel);
+    a.st = *reinterpret_cast<DState<Real> *>(h->dstate);
+    a.N = h->n; a.mode = mode; a.n_list = n_list; a.auto_reset = h->auto_reset; a.env_offset = h->env_offset;
+    a.blocks = (count + EPB - 1) / EPB;
+    a.act_stride = h->act_stride; a.obs_stride = h->obs_stride; a.info_stride = h->info_stride;
+    a.actions = reinterpret_cast<const Real *>(actions);
+    a.obs = reinterpret_cast<Real *>(obs);
+    a.reward = reinterpret_cast<Real *>(reward);
+    a.info = reinterpret_cast<Real *>(info);
+    a.done_out = done;
+    a.env_ids = env_ids; a.ref_index = ref_index;
+    a.seed = h->seed;
+    return a;
+}
+
+template <class T, typename Real>
 void launch_impl(bioim_handle_t *h, int mode, const void *actions, void *obs, void *reward, uint8_t *done, void *info,
                  const int32_t *env_ids, const int32_t *ref_index, int n_list) {
-    constexpr int EPB = BIOIM_WG / T::G;
-    int count = mode == 1 ? n_list : h->n;
-    int blocks = (count + EPB - 1) / EPB;
-    DState<Real> st = *reinterpret_cast<DState<Real> *>(h->dstate);
-    typedef SModel<T, Real> SM_t;
-    const size_t lds = lds_bytes<T, Real>();
-    const SM_t *smodel = reinterpret_cast<const SM_t *>(h->smodel);
-    hipLaunchKernelGGL((env_kernel<T, Real>), dim3(blocks), dim3(BIOIM_WG), lds, h->stream,
-                       reinterpret_cast<const DModel<Real> *>(h->model), smodel, st, h->n, mode,
-                       reinterpret_cast<const Real *>(actions), reinterpret_cast<Real *>(obs),
-                       reinterpret_cast<Real *>(reward), done, reinterpret_cast<Real *>(info), env_ids, ref_index,
-                       n_list, h->auto_reset, h->seed, h->env_offset);
+    LaunchArgs<T, Real> a = make_args<T, Real>(h, mode, actions, obs, reward, done, info, env_ids, ref_index, n_list);
+    if (a.blocks <= 0) return;
+    constexpr size_t lds = lds_bytes<T, Real>();
+    hipLaunchKernelGGL((env_kernel<T, Real>), dim3(a.blocks), dim3(BIOIM_WG), lds, h->stream, a);
 }
 
 template <class T, typename Real> int upload_smodel(bioim_handle_t *h) {
@@ -2041,6 +2079,7 @@ int bioim_create(const bioim_modelpack_t *pack, int n_envs, int device, int prec
     h->ndof = pack->ndof; h->nmuscle = pack->nmuscle; h->nact = pack->nact; h->horizon = pack->horizon;
     h->obs_dim = pack->obs_dim; h->info_dim = pack->info_dim; h->nsub = pack->nsub; h->auto_reset = 0;
     h->env_offset = 0;
+    h->act_stride = pack->nact; h->obs_stride = pack->obs_dim; h->info_stride = pack->info_dim;
     h->ops = ops;
     memcpy(&h->pack, pack, sizeof(bioim_modelpack_t));
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -2093,6 +2132,46 @@ int bioim_set_auto_reset(bioim_handle_t *h, int on) {
     return 0;
 }
 
+int bioim_set_io_strides(bioim_handle_t *h, int act_stride, int obs_stride, int info_stride) {
+    if (!h || act_stride < h->nact || obs_stride < h->obs_dim || info_stride < h->info_dim)
+        return fail(BIOIM_E_ARG, "bioim_set_io_strides: a stride is smaller than the row it holds");
+    h->act_stride = act_stride; h->obs_stride = obs_stride; h->info_stride = info_stride;
+    return 0;
+}
+
+int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs, void *reward, uint8_t *done,
+                     void *info) {
+    if (!hs || nh <= 0 || !actions || !done) return fail(BIOIM_E_ARG, "bioim_step_group: bad arguments");
+    for (int i = 0; i < nh; ++i) {
+        if (!hs[i]) return fail(BIOIM_E_ARG, "bioim_step_group: null handle");
+        if (hs[i]->device != hs[0]->device || hs[i]->precision != hs[0]->precision ||
+            hs[i]->act_stride != hs[0]->act_stride || hs[i]->obs_stride != hs[0]->obs_stride ||
+            hs[i]->info_stride != hs[0]->info_stride)
+            return fail(BIOIM_E_ARG, "bioim_step_group: handles differ in device, precision or I/O strides");
+    }
+    HIPCHK(hipSetDevice(hs[0]->device));
+    const size_t R = hs[0]->precision == 64 ? 8 : 4;
+    hipStream_t stream = hs[0]->stream;
+    /* one launch per segment, in order on the first handle's stream.  (A fused two-topology kernel
+     * was tried — workgroups [0, B0) one topology, the rest the other — and dropped: at 4096 envs
+     * each segment already fills the GPU, so it bought only the tail between launches, and its
+     * fp64 build miscompiled the second segment's muscle report) */
+    size_t off = 0;
+    for (int i = 0; i < nh; ++i) {
+        bioim_handle_t *h = hs[i];
+        hipStream_t own = h->stream;
+        h->stream = stream;
+        h->ops.launch(h, 0, (const char *)actions + off * h->act_stride * R,
+                      obs ? (char *)obs + off * h->obs_stride * R : nullptr,
+                      reward ? (char *)reward + off * R : nullptr, done + off,
+                      info ? (char *)info + off * h->info_stride * R : nullptr, nullptr, nullptr, 0);
+        h->stream = own;
+        off += (size_t)h->n;
+    }
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 int bioim_set_env_offset(bioim_handle_t *h, int offset) {
     if (!h || offset < 0) return fail(BIOIM_E_ARG, "bioim_set_env_offset: bad arguments");
     h->env_offset = offset;
@@ -2120,6 +2199,14 @@ int bioim_query(const bioim_handle_t *h, int32_t *out) {
     if (!h || !out) return fail(BIOIM_E_ARG, "bioim_query: bad arguments");
     out[0] = h->n; out[1] = h->obs_dim; out[2] = h->nact; out[3] = h->info_dim;
     out[4] = h->precision; out[5] = h->ops.lanes; out[6] = h->nsub; out[7] = bioim_state_dim(h);
+    return 0;
+}
+
+int bioim_query_launch(const bioim_handle_t *h, int32_t *out) {
+    if (!h || !out) return fail(BIOIM_E_ARG, "bioim_query_launch: bad arguments");
+    const int epb = BIOIM_WG / h->ops.lanes;
+    out[0] = h->ops.lanes; out[1] = BIOIM_WG; out[2] = epb; out[3] = (int32_t)h->ops.lds_bytes;
+    out[4] = (h->n + epb - 1) / epb;
     return 0;
 }
 

@@ -81,6 +81,18 @@ int bioim_reset(bioim_handle_t *h, const int32_t *env_ids, const int32_t *ref_in
  * same launch and their obs row is the post-reset observation. */
 int bioim_step(bioim_handle_t *h, const void *actions, void *obs, void *reward, uint8_t *done, void *info);
 int bioim_set_auto_reset(bioim_handle_t *h, int on);
+/* Row strides (in elements) of the actions / obs / info buffers this handle
+ * reads and writes (default nact, obs_dim, info_dim).  Larger strides let
+ * handles of different env IDs share padded buffers. */
+int bioim_set_io_strides(bioim_handle_t *h, int act_stride, int obs_stride, int info_stride);
+/* One env step of a mixed batch (BASELINE config C5): handle i
+ * owns rows [sum(n_<i), sum(n_<=i)) of the padded buffers (all handles on one
+ * device, same precision and strides; auto-reset per handle).  Segments are
+ * launched in order on hs[0]'s stream.  Replaces nothing in the reference
+ * (one OsimModel per Ray worker); the batch is the RLlib VectorEnv over
+ * heterogeneous sub-envs. */
+int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs, void *reward, uint8_t *done,
+                     void *info);
 /* Global index of this handle's env 0 (multi-GPU sharding): device-drawn
  * reset indices depend on the global env index, so a sharded run is
  * bit-identical to an unsharded one. */
@@ -93,6 +105,9 @@ int bioim_set_state(bioim_handle_t *h, const double *host_state);
 
 /* out[0..7] = n_envs, obs_dim, nact, info_dim, precision, lanes_per_env, nsub, state_dim */
 int bioim_query(const bioim_handle_t *h, int32_t *out);
+/* out[0..4] = lanes per env, threads per workgroup, envs per workgroup,
+ * LDS bytes per workgroup (model image + env regions), workgroups per step */
+int bioim_query_launch(const bioim_handle_t *h, int32_t *out);
 void *bioim_stream(bioim_handle_t *h);
 int bioim_set_stream(bioim_handle_t *h, void *hip_stream);
 int bioim_sync(bioim_handle_t *h);
