@@ -185,6 +185,7 @@ class EnvSpec:
     kp: Optional[List[float]] = None
     kv: Optional[List[float]] = None
     pd_coords: Optional[List[str]] = None
+    pd_vcoords: Optional[List[str]] = None   # speed coordinates (default: pd_coords)
     slow_twitch: Optional[List[float]] = None
     nsub: int = 20
     height: float = 1.80
@@ -473,6 +474,7 @@ def compile_pack(model: OsimModel, spec: EnvSpec, ref: dict) -> P.ModelPack:
     if spec.pd:
         for i, cn in enumerate(spec.pd_coords):
             pk.pd_coord[i] = cidx[cn]
+            pk.pd_vcoord[i] = cidx[(spec.pd_vcoords or spec.pd_coords)[i]]
             pk.kp[i], pk.kv[i] = spec.kp[i], spec.kv[i]
     pk.step_size = 0.01
     pk.w_imitate, pk.w_effort, pk.w_action = spec.w_imitate, spec.w_effort, spec.w_action

@@ -3,7 +3,7 @@ tests/test_modelpack.py checks sizeof against both shared libraries)."""
 import ctypes as C
 
 MAGIC = 0x4D4F4942
-VERSION = 1
+VERSION = 2
 
 MAX_COORD = 24
 MAX_CBODY = 12
@@ -107,7 +107,7 @@ class ModelPack(C.Structure):
         ('torso_body', I), ('calcn_r_body', I), ('calcn_l_body', I),
         ('n_obs_bpos', I), ('n_obs_bvel', I),
         ('obs_bpos', I * MAX_OBSBODY), ('obs_bvel', I * MAX_OBSBODY),
-        ('rw_body', I * NREFBODY), ('pd_coord', I * MAX_ACT), ('pad0', I),
+        ('rw_body', I * NREFBODY), ('pd_coord', I * MAX_ACT), ('pd_vcoord', I * MAX_ACT), ('pad0', I),
         ('step_size', D), ('w_imitate', D), ('w_effort', D), ('w_action', D),
         ('action_r_scale', D), ('max_actuation', D),
         ('total_mass', D), ('gravity', D * 3), ('height', D),

@@ -320,30 +320,34 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
 template <class T, typename Real> struct Lay {
     static constexpr int NB = T::NB, ND = T::ND > 0 ? T::ND : 1, NC = T::NC, NP = ND * (ND + 1) / 2;
     static constexpr int NMS = T::NM > T::NA ? T::NM : T::NA;
+    static constexpr int MPL = (NMS + T::G - 1) / T::G;      /* muscles (actions) per lane            */
+    static constexpr int NTL = NMS < T::G ? NMS : T::G;      /* lanes holding muscles / actuators     */
     static constexpr int NS = T::NS > 0 ? T::NS : 1, NL = T::NL > 0 ? T::NL : 1;
-    static constexpr int CJN = 3 * ND + 8;       /* per sphere: jc[ND][3], Ft3, C3 (xx xz yy zz), pad */
+    static constexpr int CJN = 10;               /* per sphere: P3, F3 (implicit), C4 (xx xz yy zz)  */
+    static constexpr int NTR = (T::TX >= 0) + (T::TY >= 0) + (T::TZ >= 0);
+    /* largest observation of the topology (target obs and GRF on) */
+    static constexpr int OBSMAX = 1 + (NC - NTR) + 2 * NC + 2 * (NC - 1) + 3 * (T::NOBP + T::NOBV) + 3 * T::NM +
+                                  6 * T::NF;
     static constexpr int KB = 0;                 /* [NB+1][18]: R9 o3 w3 vO3 (slot NB: ground)      */
     static constexpr int AL = KB + 18 * (NB + 1); /* [NB+1][6]: alpha3, aO3 (velocity-product accels) */
     static constexpr int S = AL + 6 * (NB + 1);  /* [ND][6]: Plucker columns (Omega, V at origin)   */
     static constexpr int QF = S + 6 * ND;        /* [NC] coordinate values                          */
     static constexpr int UF = QF + NC;           /* [NC] coordinate speeds                          */
-    static constexpr int IC = UF + NC;           /* [NB][10]: m, h3, J6                             */
-    static constexpr int WB = IC + 10 * NB;      /* [NB][6]: n3, f3                                 */
-    static constexpr int ICS = WB + 6 * NB;      /* subtree sums of IC                              */
-    static constexpr int WBS = ICS + 10 * NB;    /* subtree sums of WB                              */
-    static constexpr int MP = WBS + 6 * NB;      /* [NP] packed lower M (+implicit)                 */
+    static constexpr int IC = UF + NC;           /* [NB][10]: m, h3, J6; then in place: subtree sums */
+    static constexpr int WB = IC + 10 * NB;      /* [NB][6]: n3, f3; then in place: subtree sums     */
+    static constexpr int MP = WB + 6 * NB;       /* [NP] packed lower M (+implicit)                 */
     static constexpr int RHS = MP + NP;          /* [ND]                                            */
     static constexpr int CW = RHS + ND;          /* [NS][8]: F3, Mo3, active                        */
     static constexpr int LIM = CW + 8 * NS;      /* [NL][4]: f, diag add, tau add                   */
     static constexpr int U = ((LIM + 4 * NL + 1) / 2) * 2;
     static constexpr int LOC = U;                /* phase 1: [NB+1][24] joint-local data (NB: identity) */
     static constexpr int SL = LOC + 24 * (NB + 1); /* phase 1: [ND][6] joint-local Plucker columns  */
-    static constexpr int TAU = U;                /* phases 2-3: [NMS][ND] muscle/actuator slots     */
-    static constexpr int CJ = TAU + NMS * ND;    /* phases 2-3: [NS][CJN] contact slots             */
+    static constexpr int TAU = U;                /* phases 2-3: [NTL][ND] per-lane muscle/actuator torques */
+    static constexpr int CJ = TAU + NTL * ND;    /* phases 2-3: [NS][CJN] contact slots             */
     static constexpr int OBS = U;                /* report: observation staging                     */
-    static constexpr int REP = OBS + BIOIM_OBS_MAX; /* report: [NOS+1][6] body pos/vel (NOS: COM) */
-    static constexpr int U1 = 24 * (NB + 1) + 6 * ND, U2 = NMS * ND + NS * CJN;
-    static constexpr int U3 = BIOIM_OBS_MAX + 6 * (T::NOS + 1);
+    static constexpr int REP = OBS + OBSMAX;     /* report: [NOS+1][6] body pos/vel (NOS: COM)      */
+    static constexpr int U1 = 24 * (NB + 1) + 6 * ND, U2 = NTL * ND + NS * CJN;
+    static constexpr int U3 = OBSMAX + 6 * (T::NOS + 1);
     static constexpr int USZ = U1 > U2 ? (U1 > U3 ? U1 : U3) : (U2 > U3 ? U2 : U3);
     static constexpr int SIZE = ((U + USZ + 1) / 2) * 2;
 };
@@ -721,17 +725,16 @@ template <typename Real> DEV Real smooth_step_d(Real y0, Real y1, Real x0, Real 
 }
 
 /* Hunt-Crossley sphere s (this lane) vs the ground plane.  Publishes the
- * sphere's wrench about the (shifted) ground origin (CW), and for the
- * generalized force / implicit matrix: the contact-point Jacobian jc[ND][3],
- * the force Ft (normal component at the implicitly advanced position) and
- * the 3x3 implicit damping/stiffness block (h > 0), assembled per M entry
- * and per rhs row in phase 3. */
+ * sphere's wrench about the (shifted) ground origin (CW) and, for the
+ * generalized force / implicit matrix, the contact point P, the force F
+ * (normal component at the implicitly advanced position) and the 3x3
+ * implicit damping/stiffness block C (h > 0) into CJ.  Phase 3 forms the
+ * contact-point Jacobian J_d = S_d.ang x P + S_d.lin from the Plucker
+ * columns it already holds: M_lk += J_l.C J_k, rhs_d += S_d.(P x F, F). */
 template <class T, typename Real>
-DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, const Real (&S)[Lay<T, Real>::ND][6], int s, Real h) {
+DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, int s, Real h) {
     using LY = Lay<T, Real>;
-    constexpr int ND = LY::ND;
     const int cb = SM.sph_cb[s], fo = SM.sph_force[s];
-    const uint32_t mask = SM.dofmask[cb];
     const Real *kb = lds + LY::KB + 18 * cb;
     Real *cw = lds + LY::CW + 8 * s;
     Real *cj = lds + LY::CJ + LY::CJN * s;
@@ -776,16 +779,11 @@ DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, const Real (&S)[Lay<
     for (int i = 0; i < 3; ++i) { cw[i] = F[i]; cw[3 + i] = mo[i]; }
     Real kn = Real(1.5) * fH / depth * (Real(1) + Real(1.5) * SM.cf_c[fo] * vn);
     /* implicit extra force -h*Kn*v_y (Hertz force at the advanced position) */
-    cj[3 * ND] = F[0];
-    cj[3 * ND + 1] = F[1] - (h > 0 ? h * kn * vs[1] : Real(0));
-    cj[3 * ND + 2] = F[2];
 #pragma unroll
-    for (int d = 0; d < ND; ++d) {
-        Real on = (mask >> d) & 1u ? Real(1) : Real(0), j[3];
-        cross3(S[d], P, j);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) cj[3 * d + i] = on * (j[i] + S[d][3 + i]);
-    }
+    for (int i = 0; i < 3; ++i) cj[i] = P[i];
+    cj[3] = F[0];
+    cj[4] = F[1] - (h > 0 ? h * kn * vs[1] : Real(0));
+    cj[5] = F[2];
     Real cxx = 0, cxz = 0, cyy = 0, czz = 0;
     if (h > 0) {
         Real g_s, gp;
@@ -805,7 +803,14 @@ DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, const Real (&S)[Lay<
         cxz = cq * tx * tz;
         czz = ctt + cq * tz * tz;
     }
-    cj[3 * ND + 3] = cxx; cj[3 * ND + 4] = cxz; cj[3 * ND + 5] = cyy; cj[3 * ND + 6] = czz;
+    cj[6] = cxx; cj[7] = cxz; cj[8] = cyy; cj[9] = czz;
+}
+
+/* contact-point Jacobian column of a dof: S.ang x P + S.lin */
+template <typename Real> DEV void contact_jac(const Real *Sd, const Real *P, Real *j) {
+    cross3(Sd, P, j);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) j[i] += Sd[3 + i];
 }
 
 /* ------------------------------------------------------------ muscles */
@@ -976,22 +981,25 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
 
 /* ------------------------------------------------------------ dynamics */
 template <class T, typename Real> struct Dyn {
+    static constexpr int MPL = Lay<T, Real>::MPL;
     Real qdd[Lay<T, Real>::ND];
-    MState<Real> ms; /* this lane's muscle */
-    Real act, lce;   /* this lane's muscle state used (after a reset equilibrium) */
+    MState<Real> ms[MPL]; /* this lane's muscles m = lane + j*G */
+    Real act[MPL], lce[MPL]; /* their state used (after a reset equilibrium) */
     Real x0;         /* floating origin used for the published frames */
     bool ok;
 };
 
-/* Forward dynamics at (q, u, this lane's muscle state) with held controls.
+/* Forward dynamics at (q, u, this lane's muscle states) with held controls.
  * h > 0: increment of the linearly-implicit substep; h == 0: the true
  * accelerations (realize).  Leaves frames, contact wrenches and limit
- * forces published in LDS for reporting. */
+ * forces published in LDS for reporting.  Lane j-th muscle: m = lane + j*G. */
 template <class T, typename Real>
-DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *q, const Real *u, Real act, Real lce,
-                  Real control, int lane, Real *lds, Real h, bool equilibrate, Dyn<T, Real> &D) {
+DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *q, const Real *u,
+                  const Real (&act)[Lay<T, Real>::MPL], const Real (&lce)[Lay<T, Real>::MPL],
+                  const Real (&control)[Lay<T, Real>::MPL], int lane, Real *lds, Real h, bool equilibrate,
+                  Dyn<T, Real> &D) {
     using LY = Lay<T, Real>;
-    constexpr int ND = LY::ND, NP = LY::NP, NB = T::NB, G = T::G;
+    constexpr int ND = LY::ND, NP = LY::NP, NB = T::NB, G = T::G, MPL = LY::MPL;
     static_assert(NB < G && ND <= G, "lane NB writes the ground slot; one lane per dof");
     STAMP_DECL
     Real x0 = 0;
@@ -1023,7 +1031,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
     if (lane < ND) kin_column<T, Real>(SM, lds, lane);
     if (lane < NB) body_inertia<T, Real>(SM, M, lds, lane);
     wave_sync();
-    /* Plucker columns in registers for the muscle-path and contact lanes */
+    /* Plucker columns in registers for the muscle-path lanes */
     Real Sr[ND][6];
 #pragma unroll
     for (int d = 0; d < ND; ++d)
@@ -1032,49 +1040,77 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
     STAMP(2);
 
     /* ---- phase 2: lane-parallel force elements */
-    if (lane < NB) { /* subtree sums of inertia and wrench */
+    {   /* subtree sums of inertia and wrench, in place (all reads, then all writes) */
         Real ic[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, wb[6] = {0, 0, 0, 0, 0, 0};
-        sfor<0, NB>([&](auto dI) {
-            constexpr int d = decltype(dI)::value;
-            if ((T::anc[d] >> lane) & 1u) {
+        if (lane < NB) {
+            sfor<0, NB>([&](auto dI) {
+                constexpr int d = decltype(dI)::value;
+                if ((T::anc[d] >> lane) & 1u) {
 #pragma unroll
-                for (int i = 0; i < 10; ++i) ic[i] += lds[LY::IC + 10 * d + i];
+                    for (int i = 0; i < 10; ++i) ic[i] += lds[LY::IC + 10 * d + i];
 #pragma unroll
-                for (int i = 0; i < 6; ++i) wb[i] += lds[LY::WB + 6 * d + i];
-            }
-        });
+                    for (int i = 0; i < 6; ++i) wb[i] += lds[LY::WB + 6 * d + i];
+                }
+            });
+        }
+        wave_sync();
+        if (lane < NB) {
 #pragma unroll
-        for (int i = 0; i < 10; ++i) lds[LY::ICS + 10 * lane + i] = ic[i];
+            for (int i = 0; i < 10; ++i) lds[LY::IC + 10 * lane + i] = ic[i];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) lds[LY::WBS + 6 * lane + i] = wb[i];
+            for (int i = 0; i < 6; ++i) lds[LY::WB + 6 * lane + i] = wb[i];
+        }
     }
     STAMP(3);
     if constexpr (T::NM > 0) {
-        if (lane < T::NM) {
-            const SMuscle<Real> &mu = SM.mus[lane];
-            Real L, dLdq[ND];
-            muscle_path<T, Real>(SM, mu, lds, Sr, L, dLdq);
-            STAMP(4);
-            if (equilibrate) { /* reset: default activation, static fiber equilibrium */
-                act = mu.default_act;
-                lce = muscle_equilibrium<T, Real>(SM, mu, act, L);
-            }
-            D.act = act;
-            D.lce = lce;
-            muscle_eval<T, Real>(SM, mu, act, lce, control, L, D.ms.vN, D.ms);
+        Real tau[ND];
 #pragma unroll
-            for (int d = 0; d < ND; ++d) lds[LY::TAU + ND * lane + d] = -D.ms.Ft * dLdq[d];
+        for (int d = 0; d < ND; ++d) tau[d] = 0;
+        sfor<0, MPL>([&](auto jI) {
+            constexpr int j = decltype(jI)::value;
+            const int m = lane + j * G;
+            if (m < T::NM) {
+                const SMuscle<Real> &mu = SM.mus[m];
+                Real L, dLdq[ND];
+                muscle_path<T, Real>(SM, mu, lds, Sr, L, dLdq);
+                STAMP(4);
+                Real a_ = act[j], l_ = lce[j];
+                if (equilibrate) { /* reset: default activation, static fiber equilibrium */
+                    a_ = mu.default_act;
+                    l_ = muscle_equilibrium<T, Real>(SM, mu, a_, L);
+                }
+                D.act[j] = a_;
+                D.lce[j] = l_;
+                muscle_eval<T, Real>(SM, mu, a_, l_, control[j], L, D.ms[j].vN, D.ms[j]);
+#pragma unroll
+                for (int d = 0; d < ND; ++d) tau[d] += -D.ms[j].Ft * dLdq[d];
+            }
+        });
+        if (lane < LY::NTL) {
+#pragma unroll
+            for (int d = 0; d < ND; ++d) lds[LY::TAU + ND * lane + d] = tau[d];
         }
     } else {
-        if (lane < T::NA) {
-            int ad = SM.act_dof[lane];
-            Real f = control * SM.ca_opt[lane];
+        Real tau[ND];
 #pragma unroll
-            for (int d = 0; d < ND; ++d) lds[LY::TAU + ND * lane + d] = (d == ad) ? f : Real(0);
+        for (int d = 0; d < ND; ++d) tau[d] = 0;
+        sfor<0, MPL>([&](auto jI) {
+            constexpr int j = decltype(jI)::value;
+            const int m = lane + j * G;
+            if (m < T::NA) {
+                const int ad = SM.act_dof[m];
+                const Real f = control[j] * SM.ca_opt[m];
+#pragma unroll
+                for (int d = 0; d < ND; ++d) tau[d] += (d == ad) ? f : Real(0);
+            }
+        });
+        if (lane < LY::NTL) {
+#pragma unroll
+            for (int d = 0; d < ND; ++d) lds[LY::TAU + ND * lane + d] = tau[d];
         }
     }
     STAMP(5);
-    if (lane < T::NS) contact_lane<T, Real>(SM, lds, Sr, lane, h);
+    if (lane < T::NS) contact_lane<T, Real>(SM, lds, lane, h);
     STAMP(6);
     if (lane < T::NL) {
         int cc = SM.lim_coord[lane];
@@ -1101,9 +1137,10 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
     /* ---- phase 3: mass-matrix entries and right-hand side, fixed-order sums */
     for (int e = lane; e < NP; e += G) {
         int l = SM.e_l[e], k = SM.e_k[e], c = SM.e_c[e];
+        const Real *Sl = lds + LY::S + 6 * l, *Sk = lds + LY::S + 6 * k;
         Real v = 0;
         if (c >= 0) {
-            const Real *Sl = lds + LY::S + 6 * l, *Sk = lds + LY::S + 6 * k, *ic = lds + LY::ICS + 10 * c;
+            const Real *ic = lds + LY::IC + 10 * c;
             Real Lm[3], Pm[3], t[3];
             symv(ic + 4, Sl, Lm);
             cross3(ic + 1, Sl + 3, t);
@@ -1115,15 +1152,20 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
             v = dot3(Sk, Lm) + dot3(Sk + 3, Pm);
         }
         if (h > 0) {
-            /* branch-free: every slot is read (independent loads), inactive
-             * spheres (stale slots) are dropped by a select */
-#pragma unroll
-            for (int s = 0; s < T::NS; ++s) {
-                const Real *cj = lds + LY::CJ + LY::CJN * s, *C = cj + 3 * ND + 3;
-                const Real *jl = cj + 3 * l, *jk = cj + 3 * k;
+            /* implicit contact: J_l.C J_k per sphere whose body both dofs move;
+             * every slot is read (independent loads), inactive spheres (stale
+             * slots) are dropped by a select */
+            sfor<0, T::NS>([&](auto sI) {
+                constexpr int sp = decltype(sI)::value;
+                constexpr unsigned msk = T::dofmask[T::sphere_cb[sp]];
+                const Real *cj = lds + LY::CJ + LY::CJN * sp, *C = cj + 6;
+                Real jl[3], jk[3];
+                contact_jac(Sl, cj, jl);
+                contact_jac(Sk, cj, jk);
                 Real term = jl[0] * (C[0] * jk[0] + C[1] * jk[2]) + jl[1] * (C[2] * jk[1]) + jl[2] * (C[1] * jk[0] + C[3] * jk[2]);
-                v += lds[LY::CW + 8 * s + 6] > 0 ? term : Real(0);
-            }
+                const bool on = lds[LY::CW + 8 * sp + 6] > 0 && ((msk >> l) & (msk >> k) & 1u);
+                v += on ? term : Real(0);
+            });
             if (l == k)
 #pragma unroll
                 for (int li = 0; li < T::NL; ++li)
@@ -1132,17 +1174,19 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
         lds[LY::MP + e] = v;
     }
     if (lane < ND) {
-        const Real *Sd = lds + LY::S + 6 * lane, *wb = lds + LY::WBS + 6 * SM.dof_cb[lane];
+        const Real *Sd = lds + LY::S + 6 * lane, *wb = lds + LY::WB + 6 * SM.dof_cb[lane];
         Real r = -(dot3(Sd, wb) + dot3(Sd + 3, wb + 3));
 #pragma unroll
-        for (int m = 0; m < LY::NMS; ++m)
-            if (m < (T::NM > 0 ? T::NM : T::NA)) r += lds[LY::TAU + ND * m + lane];
-#pragma unroll
-        for (int s = 0; s < T::NS; ++s) {
-            const Real *cj = lds + LY::CJ + LY::CJN * s;
-            Real term = dot3(cj + 3 * lane, cj + 3 * ND);
-            r += lds[LY::CW + 8 * s + 6] > 0 ? term : Real(0);
-        }
+        for (int m = 0; m < LY::NTL; ++m) r += lds[LY::TAU + ND * m + lane];
+        sfor<0, T::NS>([&](auto sI) {
+            constexpr int sp = decltype(sI)::value;
+            constexpr unsigned msk = T::dofmask[T::sphere_cb[sp]];
+            const Real *cj = lds + LY::CJ + LY::CJN * sp;
+            Real jd[3];
+            contact_jac(Sd, cj, jd);
+            const Real term = dot3(jd, cj + 3);
+            r += (lds[LY::CW + 8 * sp + 6] > 0 && ((msk >> lane) & 1u)) ? term : Real(0);
+        });
 #pragma unroll
         for (int li = 0; li < T::NL; ++li)
             if (SM.lim_dof[li] == lane) r += lds[LY::LIM + 4 * li + 2];
@@ -1290,21 +1334,31 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         env = gidx;
     }
     const int H = M.horizon;
+    constexpr int MPL = LY::MPL;                  /* muscles / actions per lane: m = lane + j*G */
+    constexpr int CPL = (T::NC + G - 1) / G;      /* coordinates per lane (report)              */
     Dyn<T, Real> D;
-    D.ms.vN = 0;
+#pragma unroll
+    for (int j = 0; j < MPL; ++j) D.ms[j].vN = 0;
     Real q[ND], u[ND];
 #pragma unroll
     for (int d = 0; d < ND; ++d) { q[d] = st.q[(size_t)d * N + env]; u[d] = st.u[(size_t)d * N + env]; }
     double t = st.t[env];
     int istep = st.istep[env], has_last = st.has_last[env], resets = st.resets[env];
     Real old_px = st.old_px[env];
-    Real act = 0, lce = 0, control = 0, curr = 0, last = 0, hist[BIOIM_MAX_HORIZON];
-    if (NM > 0 && lane < NM) { act = st.act[(size_t)lane * N + env]; lce = st.lce[(size_t)lane * N + env]; }
-    if (lane < NA) {
-        last = st.last[(size_t)lane * N + env];
+    Real act[MPL], lce[MPL], control[MPL], curr[MPL], last[MPL], hist[MPL][BIOIM_MAX_HORIZON];
 #pragma unroll
-        for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
-            hist[hh] = hh < H ? st.hist[((size_t)hh * NA + lane) * N + env] : Real(0);
+    for (int j = 0; j < MPL; ++j) {
+        const int m = lane + j * G;
+        act[j] = 0; lce[j] = 0; control[j] = 0; curr[j] = 0; last[j] = 0;
+        if (NM > 0 && m < NM) { act[j] = st.act[(size_t)m * N + env]; lce[j] = st.lce[(size_t)m * N + env]; }
+#pragma unroll
+        for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh) hist[j][hh] = 0;
+        if (m < NA) {
+            last[j] = st.last[(size_t)m * N + env];
+#pragma unroll
+            for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
+                hist[j][hh] = hh < H ? st.hist[((size_t)hh * NA + m) * N + env] : Real(0);
+        }
     }
     int done = 0;
     Real rew = 0, inf[5] = {0, 0, 0, 0, 0};
@@ -1316,45 +1370,69 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     Real dt = 0;
     if (mode == 0) {
         /* ---- action pre-processing (Env.step) */
-        Real raw = lane < NA ? actions[(size_t)env * a.act_stride + lane] : Real(0);
-        bool anynan = group_any<G>(lane < NA && isnan(raw));
-        Real a = anynan ? Real(0) : raw;
+        Real raw[MPL];
+        bool nan_here = false;
+#pragma unroll
+        for (int j = 0; j < MPL; ++j) {
+            const int m = lane + j * G;
+            raw[j] = m < NA ? actions[(size_t)env * a.act_stride + m] : Real(0);
+            nan_here = nan_here || (m < NA && isnan(raw[j]));
+        }
+        const bool anynan = group_any<G>(nan_here);
+        Real av[MPL];
+#pragma unroll
+        for (int j = 0; j < MPL; ++j) av[j] = anynan ? Real(0) : raw[j];
         if constexpr ((T::FLAGS & BIOIM_ENV_PD) != 0) {
             if (!anynan) {
                 Real qf[T::NC], uf[T::NC];
                 fill_coords<T, Real>(M, q, u, qf, uf);
-                Real xq = 0, xu = 0;
-                sfor<0, NA>([&](auto iI) {
-                    constexpr int i = decltype(iI)::value;
-                    if (lane == i) { xq = qf[T::pd_coord[i]]; xu = uf[T::pd_coord[i]]; }
-                });
-                if (lane < NA) a = SM.kp[lane] * (raw - xq) - SM.kv[lane] * xu;
+#pragma unroll
+                for (int j = 0; j < MPL; ++j) {
+                    const int m = lane + j * G;
+                    Real xq = 0, xu = 0;
+                    sfor<0, NA>([&](auto iI) {
+                        constexpr int i = decltype(iI)::value;
+                        if (m == i) { xq = qf[T::pd_coord[i]]; xu = uf[T::pd_vcoord[i]]; }
+                    });
+                    if (m < NA) av[j] = SM.kp[m] * (raw[j] - xq) - SM.kv[m] * xu;
+                }
             }
         }
-        if (!has_last) {
-            last = a;
+        bool pnan_here = false;
 #pragma unroll
-            for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh) hist[hh] = a;
+        for (int j = 0; j < MPL; ++j) {
+            const int m = lane + j * G;
+            if (!has_last) {
+                last[j] = av[j];
+#pragma unroll
+                for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh) hist[j][hh] = av[j];
+            }
+            /* fixed-trip loops keep the history in registers */
+#pragma unroll
+            for (int hh = 0; hh + 1 < BIOIM_MAX_HORIZON; ++hh)
+                if (hh + 1 < H) hist[j][hh] = hist[j][hh + 1];
+#pragma unroll
+            for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
+                if (hh == H - 1) hist[j][hh] = av[j];
+            Real sm = 0;
+#pragma unroll
+            for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
+                if (hh < H) sm += hist[j][hh];
+            curr[j] = sm / Real(H);
+            const Real phys = (M.env_flags & BIOIM_ENV_RAW_ACTION) ? av[j] : curr[j];
+            pnan_here = pnan_here || (m < NA && isnan(phys));
+            control[j] = phys;
         }
         has_last = 1;
-        /* fixed-trip loops keep the history in registers */
+        const bool pnan = group_any<G>(pnan_here);
 #pragma unroll
-        for (int hh = 0; hh + 1 < BIOIM_MAX_HORIZON; ++hh)
-            if (hh + 1 < H) hist[hh] = hist[hh + 1];
-#pragma unroll
-        for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
-            if (hh == H - 1) hist[hh] = a;
-        Real s = 0;
-#pragma unroll
-        for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
-            if (hh < H) s += hist[hh];
-        curr = s / Real(H);
-        Real phys = (M.env_flags & BIOIM_ENV_RAW_ACTION) ? a : curr;
-        bool pnan = group_any<G>(lane < NA && isnan(phys));
-        Real lo = NM > 0 ? Real(0) : SM.ca_min[lane < NA ? lane : 0];
-        Real hi = NM > 0 ? Real(1) : SM.ca_max[lane < NA ? lane : 0];
-        Real v = pnan ? Real(0) : phys;
-        control = lane < NA ? (v < lo ? lo : (v > hi ? hi : v)) : Real(0);
+        for (int j = 0; j < MPL; ++j) {
+            const int m = lane + j * G, ms = m < NA ? m : 0;
+            const Real lo = NM > 0 ? Real(0) : SM.ca_min[ms];
+            const Real hi = NM > 0 ? Real(1) : SM.ca_max[ms];
+            const Real v = pnan ? Real(0) : control[j];
+            control[j] = m < NA ? (v < lo ? lo : (v > hi ? hi : v)) : Real(0);
+        }
         /* ---- integrate to step_size * istep (semi-implicit substeps) */
         istep += 1;
         double tf = M.step_size * (double)istep;
@@ -1383,7 +1461,8 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             t = M.ref_time[r];
             istep = M.ref_istep[r];
             has_last = 0;
-            control = 0;
+#pragma unroll
+            for (int j = 0; j < MPL; ++j) control[j] = 0;
             resets += 1;
         }
         {
@@ -1399,18 +1478,28 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         if (sub) {
 #pragma unroll
             for (int d = 0; d < ND; ++d) { u[d] += dt * D.qdd[d]; q[d] += dt * u[d]; }
-            if (NM > 0 && lane < NM) {
-                act += dt * D.ms.dadt;
-                if (!D.ms.clamped) {
-                    Real ln = lce + dt * D.ms.vce / (Real(1) - dt * D.ms.dvdl);
-                    lce = ln < SM.mus[lane].lmin ? SM.mus[lane].lmin : ln;
+            if constexpr (NM > 0) {
+#pragma unroll
+                for (int j = 0; j < MPL; ++j) {
+                    const int m = lane + j * G;
+                    if (m < NM) {
+                        act[j] += dt * D.ms[j].dadt;
+                        if (!D.ms[j].clamped) {
+                            Real ln = lce[j] + dt * D.ms[j].vce / (Real(1) - dt * D.ms[j].dvdl);
+                            lce[j] = ln < SM.mus[m].lmin ? SM.mus[m].lmin : ln;
+                        }
+                    }
                 }
             }
             --remaining;
             continue;
         }
         if (eq) {
-            if (NM > 0 && lane < NM) { act = D.act; lce = D.lce; }
+            if constexpr (NM > 0) {
+#pragma unroll
+                for (int j = 0; j < MPL; ++j)
+                    if (lane + j * G < NM) { act[j] = D.act[j]; lce[j] = D.lce[j]; }
+            }
             pending_reset = false;
             reported_reset = true;
         }
@@ -1432,21 +1521,24 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             ob[0] = Real(ph - floor(ph));
         }
         const int obody = OL::body(tgt);
-        if (lane < T::NC) {
-            const int c = lane;
-            const bool trans = c == T::TX || c == T::TY || c == T::TZ;
-            const int qi = c - (T::TX >= 0 && T::TX < c) - (T::TY >= 0 && T::TY < c) - (T::TZ >= 0 && T::TZ < c);
-            if (!trans) ob[OL::QPOS + qi] = lds[LY::QF + c];
-            ob[OL::QVEL + c] = lds[LY::UF + c];
-            const int dc = SM.coord_dof[c];
-            Real acc = 0;
 #pragma unroll
-            for (int d = 0; d < ND; ++d) acc = dc == d ? D.qdd[d] : acc;
-            ob[OL::QACC + c] = acc;
-            if (tgt && c != T::TX) {
-                const int r1 = clamp_row(istep + 1, M.nrows), ti = c - (T::TX >= 0 && T::TX < c);
-                ob[OL::TGT + ti] = M.ref_q[r1][c];
-                ob[OL::TGT + (T::NC - 1) + ti] = M.ref_u[r1][c];
+        for (int jc = 0; jc < CPL; ++jc) {
+            const int c = lane + jc * G;
+            if (c < T::NC) {
+                const bool trans = c == T::TX || c == T::TY || c == T::TZ;
+                const int qi = c - (T::TX >= 0 && T::TX < c) - (T::TY >= 0 && T::TY < c) - (T::TZ >= 0 && T::TZ < c);
+                if (!trans) ob[OL::QPOS + qi] = lds[LY::QF + c];
+                ob[OL::QVEL + c] = lds[LY::UF + c];
+                const int dc = SM.coord_dof[c];
+                Real acc = 0;
+#pragma unroll
+                for (int d = 0; d < ND; ++d) acc = dc == d ? D.qdd[d] : acc;
+                ob[OL::QACC + c] = acc;
+                if (tgt && c != T::TX) {
+                    const int r1 = clamp_row(istep + 1, M.nrows), ti = c - (T::TX >= 0 && T::TX < c);
+                    ob[OL::TGT + ti] = M.ref_q[r1][c];
+                    ob[OL::TGT + (T::NC - 1) + ti] = M.ref_u[r1][c];
+                }
             }
         }
         if (lane < T::NOBP) {
@@ -1460,10 +1552,14 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         }
         const int omus = obody + 3 * T::NOBP + 3 * T::NOBV;
         if constexpr (NM > 0) {
-            if (lane < NM) {
-                ob[omus + 3 * lane] = D.ms.act;
-                ob[omus + 3 * lane + 1] = D.ms.lce;
-                ob[omus + 3 * lane + 2] = D.ms.vce;
+#pragma unroll
+            for (int j = 0; j < MPL; ++j) {
+                const int m = lane + j * G;
+                if (m < NM) {
+                    ob[omus + 3 * m] = D.ms[j].act;
+                    ob[omus + 3 * m + 1] = D.ms[j].lce;
+                    ob[omus + 3 * m + 2] = D.ms[j].vce;
+                }
             }
         }
         if (grf && lane < T::NF) {
@@ -1493,9 +1589,13 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         {
             const int r = clamp_row(istep, M.nrows);
             Real e2 = 0;
-            if (lane < T::NC) {
-                Real e = lds[LY::QF + lane] - M.ref_q[r][lane];
-                e2 = e * e;
+#pragma unroll
+            for (int jc = 0; jc < CPL; ++jc) {
+                const int c = lane + jc * G;
+                if (c < T::NC) {
+                    Real e = lds[LY::QF + c] - M.ref_q[r][c];
+                    e2 += e * e;
+                }
             }
             const Real qerr = group_sum<G>(e2) / Real(T::NC);
             Real eb = 0;
@@ -1518,34 +1618,45 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             Real foot_r = Real(0.5) * exp(Real(-20) * err_r);
             Real foot_l = Real(0.5) * exp(Real(-20) * err_l);
             Real pelvis_x = px;
-            Real da = lane < NA ? curr - last : Real(0);
-            Real action_r = exp(-M.action_r_scale * sqrt(group_sum<G>(da * da)));
+            Real da2 = 0;
+#pragma unroll
+            for (int j = 0; j < MPL; ++j) {
+                const Real da = lane + j * G < NA ? curr[j] - last[j] : Real(0);
+                da2 += da * da;
+            }
+            Real action_r = exp(-M.action_r_scale * sqrt(group_sum<G>(da2)));
             Real effort, a_error = 0;
             if constexpr (NM > 0) {
-                Real an = lane < NM ? D.ms.act * D.ms.act : Real(0);
-                a_error = exp(Real(-2) * sqrt(group_sum<G>(an)));
-                Real cot = 0;
-                if (lane < NM) {
-                    const SMuscle<Real> &mu = SM.mus[lane];
-                    Real l = mu.slow, ex = control, aa = D.ms.act, hp = Real(0.5 * 3.14159265358979323846);
-                    Real se, ce, sa, ca;
-                    sincos_rt(hp * ex, se, ce);
-                    sincos_rt(hp * aa, sa, ca);
-                    Real fa = Real(40) * l * se + Real(133) * (Real(1) - l) * (Real(1) - ce);
-                    Real fm = Real(74) * l * sa + Real(111) * (Real(1) - l) * (Real(1) - ca);
-                    Real ln = D.ms.lce * mu.inv_lopt, vv = D.ms.vce;
-                    Real g = 0;
-                    if (ln < Real(0.5)) g = Real(0.5);
-                    else if (ln < Real(1)) g = ln;
-                    else if (ln < Real(1.5)) g = Real(-2) * ln + Real(3);
-                    Real es = fmax(Real(0), Real(0.25) * D.ms.Ff * -vv);
-                    Real ew = fmax(Real(0), D.ms.Fa * -vv);
-                    cot = mu.mass * fa + mu.mass * g * fm + es + ew;
+                Real an = 0, cot = 0;
+#pragma unroll
+                for (int j = 0; j < MPL; ++j) {
+                    const int m = lane + j * G;
+                    if (m < NM) {
+                        an += D.ms[j].act * D.ms[j].act;
+                        const SMuscle<Real> &mu = SM.mus[m];
+                        Real l = mu.slow, ex = control[j], aa = D.ms[j].act, hp = Real(0.5 * 3.14159265358979323846);
+                        Real se, ce, sa, ca;
+                        sincos_rt(hp * ex, se, ce);
+                        sincos_rt(hp * aa, sa, ca);
+                        Real fa = Real(40) * l * se + Real(133) * (Real(1) - l) * (Real(1) - ce);
+                        Real fm = Real(74) * l * sa + Real(111) * (Real(1) - l) * (Real(1) - ca);
+                        Real ln = D.ms[j].lce * mu.inv_lopt, vv = D.ms[j].vce;
+                        Real g = 0;
+                        if (ln < Real(0.5)) g = Real(0.5);
+                        else if (ln < Real(1)) g = ln;
+                        else if (ln < Real(1.5)) g = Real(-2) * ln + Real(3);
+                        Real es = fmax(Real(0), Real(0.25) * D.ms[j].Ff * -vv);
+                        Real ew = fmax(Real(0), D.ms[j].Fa * -vv);
+                        cot += mu.mass * fa + mu.mass * g * fm + es + ew;
+                    }
                 }
+                a_error = exp(Real(-2) * sqrt(group_sum<G>(an)));
                 cot = group_sum<G>(cot) + Real(1.51) * M.total_mass;
                 effort = cot / (Real(20) * Real(NM * NM));
             } else {
-                Real cn = lane < NA ? curr * curr : Real(0);
+                Real cn = 0;
+#pragma unroll
+                for (int j = 0; j < MPL; ++j) cn += lane + j * G < NA ? curr[j] * curr[j] : Real(0);
                 effort = sqrt(group_sum<G>(cn)) / (M.max_actuation * Real(NA * NA));
             }
             Real effort_r = exp(-effort / fmax(pelvis_x - old_px + Real(1), Real(1)));
@@ -1553,7 +1664,8 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             if constexpr ((T::FLAGS & BIOIM_ENV_REWARD_FEET) != 0) imit *= (foot_l + foot_r);
             rew = (Real(0.5) + M.w_imitate) * imit + M.w_effort * effort_r + M.w_action * action_r;
             inf[0] = position_r; inf[1] = com_r; inf[2] = foot_l; inf[3] = foot_r; inf[4] = a_error;
-            last = curr;
+#pragma unroll
+            for (int j = 0; j < MPL; ++j) last[j] = curr[j];
             old_px = pelvis_x;
             /* is_done (muscle_walking_imitation_env2D.py:237-265) */
             const Real torso_y = lds[LY::REP + 6 * T::TORSO + 1];
@@ -1615,12 +1727,16 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         st.q[(size_t)lane * N + env] = qv;
         st.u[(size_t)lane * N + env] = uv;
     }
-    if (NM > 0 && lane < NM) { st.act[(size_t)lane * N + env] = act; st.lce[(size_t)lane * N + env] = lce; }
-    if (lane < NA) {
-        st.last[(size_t)lane * N + env] = last;
 #pragma unroll
-        for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
-            if (hh < H) st.hist[((size_t)hh * NA + lane) * N + env] = hist[hh];
+    for (int j = 0; j < MPL; ++j) {
+        const int m = lane + j * G;
+        if (NM > 0 && m < NM) { st.act[(size_t)m * N + env] = act[j]; st.lce[(size_t)m * N + env] = lce[j]; }
+        if (m < NA) {
+            st.last[(size_t)m * N + env] = last[j];
+#pragma unroll
+            for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
+                if (hh < H) st.hist[((size_t)hh * NA + m) * N + env] = hist[j][hh];
+        }
     }
 }
 
@@ -1867,7 +1983,8 @@ template <class T> bool topology_matches(const bioim_modelpack_t &p) {
         if (p.limit[l].dof != T::limit_dof[l] || p.limit[l].coord != T::limit_coord[l]) return false;
     if (p.nmuscle == 0)
         for (int a = 0; a < T::NA; ++a)
-            if (p.coordact[a].dof != T::act_dof[a] || p.pd_coord[a] != T::pd_coord[a]) return false;
+            if (p.coordact[a].dof != T::act_dof[a] || p.pd_coord[a] != T::pd_coord[a] || p.pd_vcoord[a] != T::pd_vcoord[a])
+                return false;
     for (int b = 0; b < T::NOBP; ++b)
         if (p.obs_bpos[b] != T::obs_bpos[b]) return false;
     for (int b = 0; b < T::NOBV; ++b)
@@ -1954,6 +2071,7 @@ template <class T, typename Real> int upload_smodel(bioim_handle_t *h) {
 
 template <class T> bool pick(const bioim_modelpack_t &p, int precision, Ops &ops) {
     if (!topology_matches<T>(p)) return false;
+    if (p.obs_dim > Lay<T, double>::OBSMAX) return false;
     ops.lanes = T::G;
     if (precision == 64) {
         ops.launch = &launch_impl<T, double>;

@@ -147,6 +147,7 @@ def emit_topology(struct, pk, lanes):
     s += _carr('limit_coord', [pk.limit[i].coord for i in range(pk.nlimit)])
     s += _carr('act_dof', [pk.coordact[i].dof for i in range(pk.ncoordact)] if pk.ncoordact else [-1])
     s += _carr('pd_coord', [pk.pd_coord[i] for i in range(pk.nact)])
+    s += _carr('pd_vcoord', [pk.pd_vcoord[i] for i in range(pk.nact)])
     s += _carr('obs_bpos', [pk.obs_bpos[i] for i in range(pk.n_obs_bpos)])
     s += _carr('obs_bvel', [pk.obs_bvel[i] for i in range(pk.n_obs_bvel)])
     s += _carr('rw_body', [pk.rw_body[i] for i in range(9)])
@@ -173,7 +174,9 @@ def write_topologies(packs):
             continue
         struct = 'Topo_' + env_id.replace('-', '_')
         seen[sig] = struct
-        lanes = 16 if max(pk.nmuscle, pk.nact, pk.ncoord) <= 16 else 32
+        # 16 lanes per env (4 envs per wave): one lane per body, dof and reported body; muscles,
+        # actions and coordinates beyond 16 take a second pass on the same lanes
+        lanes = 16 if pk.ncbody < 16 and pk.ndof <= 16 and pk.nosbody < 16 else 32
         out.append(emit_topology(struct, pk, lanes))
         names.append((env_id, struct))
     out.append('#define BIOIM_FOR_EACH_TOPOLOGY(X) \\')

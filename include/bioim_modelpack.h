@@ -24,7 +24,7 @@
 #include <stdint.h>
 
 #define BIOIM_PACK_MAGIC   0x4D4F4942u /* "BIOM" */
-#define BIOIM_PACK_VERSION 1
+#define BIOIM_PACK_VERSION 2
 
 #define BIOIM_MAX_COORD    24
 #define BIOIM_MAX_CBODY    12
@@ -177,7 +177,10 @@ typedef struct {
     int32_t obs_bpos[BIOIM_MAX_OBSBODY];   /* OpenSim body index, -1 = center of mass */
     int32_t obs_bvel[BIOIM_MAX_OBSBODY];
     int32_t rw_body[BIOIM_NREFBODY];       /* sim body per ref slot, -1 = center of mass */
-    int32_t pd_coord[BIOIM_MAX_ACT];       /* PD: coordinate per action entry          */
+    int32_t pd_coord[BIOIM_MAX_ACT];       /* PD: position coordinate per action entry */
+    int32_t pd_vcoord[BIOIM_MAX_ACT];      /* PD: speed coordinate per action entry (the 3D torque
+                                              envs index q and q' differently,
+                                              torque_walking_imitation_env3D.py:130-131) */
     int32_t pad0;
 
     double  step_size;
