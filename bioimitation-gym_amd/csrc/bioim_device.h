@@ -117,7 +117,7 @@ struct SModel {
     /* coordinate actuators / PD gains (lane = actuator) */
     Real ca_opt[D::NAD], ca_min[D::NAD], ca_max[D::NAD], kp[D::NAD], kv[D::NAD];
     /* index tables */
-    int32_t coord_dof[D::NCD], dof_cb[D::NDD];
+    int32_t coord_dof[D::NCD], dof_cb[D::NDD], dof_coord[D::NDD];
     int32_t e_l[D::NP], e_k[D::NP], e_c[D::NP]; /* packed-lower M entry -> (row, col, subtree body) */
     uint32_t dofmask[T::NB];
     /* OpenSim bodies reported in observations / rewards (lane = body) */

@@ -98,6 +98,11 @@ template <int G, typename Real> DEV Real group_sum(Real x) {
     for (int off = G / 2; off >= 1; off >>= 1) x += __shfl_xor(x, off, G);
     return x;
 }
+template <int G, typename Real> DEV Real group_max(Real x) {
+#pragma unroll
+    for (int off = G / 2; off >= 1; off >>= 1) x = fmax(x, __shfl_xor(x, off, G));
+    return x;
+}
 template <int G> DEV bool group_any(bool p) {
     unsigned long long b = __ballot(p);
     int base = (threadIdx.x & 63) & ~(G - 1);
@@ -378,15 +383,22 @@ DEV void wave_sync() {
 
 template <int I> DEV constexpr int tri(int k, int l) { return k * (k + 1) / 2 + l; }
 
-/* coordinate values/speeds (locked: default / 0) */
+/* publish the coordinate values/speeds to LDS (QF/UF): dof lane d writes its
+ * coordinate, lane 0 the locked coordinates (default value, zero speed) */
 template <class T, typename Real>
-DEV void fill_coords(const DModel<Real> &M, const Real *q, const Real *u, Real *qf, Real *uf) {
-    sfor<0, T::NC>([&](auto cI) {
-        constexpr int c = decltype(cI)::value;
-        constexpr int d = T::coord_dof[c];
-        if constexpr (d >= 0) { qf[c] = q[d]; uf[c] = u[d]; }
-        else { qf[c] = M.coord_default[c]; uf[c] = 0; }
-    });
+DEV void publish_coords(const DModel<Real> &M, const SModel<T, Real> &SM, Real *lds, int lane, Real qd, Real ud) {
+    using LY = Lay<T, Real>;
+    if (lane < T::ND) {
+        const int c = SM.dof_coord[lane];
+        lds[LY::QF + c] = qd;
+        lds[LY::UF + c] = ud;
+    }
+    if (lane == 0) {
+        sfor<0, T::NC>([&](auto cI) {
+            constexpr int c = decltype(cI)::value;
+            if constexpr (T::coord_dof[c] < 0) { lds[LY::QF + c] = M.coord_default[c]; lds[LY::UF + c] = 0; }
+        });
+    }
 }
 
 /* ---------------------------------------------------------- kinematics
@@ -900,9 +912,9 @@ DEV Real muscle_equilibrium(const SModel<T, Real> &SM, const SMuscle<Real> &mu, 
  * from registers (loaded once per dynamics call).  Fixed trip count over
  * the topology's maximum point count; only the point indices that can be
  * conditional / moving (compile-time masks) carry that code. */
-template <class T, typename Real>
-DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const Real *lds,
-                     const Real (&S)[Lay<T, Real>::ND][6], Real &L, Real *dLdq) {
+template <class T, typename Real, class SA>
+DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const Real *lds, const SA &S, Real &L,
+                     Real *dLdq) {
     using LY = Lay<T, Real>;
     const Real *ldsq = lds + LY::QF;
     L = 0;
@@ -918,7 +930,9 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
 #pragma unroll
         for (int d = 0; d < T::ND; ++d) {
             Real on = (maskp >> d) & 1u ? Real(1) : Real(0);
-            dLdq[d] += on * (dot3(S[d], mo) + dot3(S[d] + 3, g)) + (mdofp == d ? dot3(g, dPp) : Real(0));
+            const Real sm = S(d, 0) * mo[0] + S(d, 1) * mo[1] + S(d, 2) * mo[2];
+            const Real sg = S(d, 3) * g[0] + S(d, 4) * g[1] + S(d, 5) * g[2];
+            dLdq[d] += on * (sm + sg) + (mdofp == d ? dot3(g, dPp) : Real(0));
         }
     };
     const int npt = mu.npt;
@@ -982,7 +996,7 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
 /* ------------------------------------------------------------ dynamics */
 template <class T, typename Real> struct Dyn {
     static constexpr int MPL = Lay<T, Real>::MPL;
-    Real qdd[Lay<T, Real>::ND];
+    Real qdd;        /* this lane's dof (lane < ND): generalized acceleration / substep increment */
     MState<Real> ms[MPL]; /* this lane's muscles m = lane + j*G */
     Real act[MPL], lce[MPL]; /* their state used (after a reset equilibrium) */
     Real x0;         /* floating origin used for the published frames */
@@ -990,11 +1004,12 @@ template <class T, typename Real> struct Dyn {
 };
 
 /* Forward dynamics at (q, u, this lane's muscle states) with held controls.
- * h > 0: increment of the linearly-implicit substep; h == 0: the true
- * accelerations (realize).  Leaves frames, contact wrenches and limit
- * forces published in LDS for reporting.  Lane j-th muscle: m = lane + j*G. */
+ * Lane d < ND owns dof d (qd, ud in, D.qdd out); lane's j-th muscle is
+ * m = lane + j*G.  h > 0: increment of the linearly-implicit substep;
+ * h == 0: the true accelerations (realize).  Leaves coordinates, frames,
+ * contact wrenches, limit forces and q'' (RHS slots) published in LDS. */
 template <class T, typename Real>
-DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *q, const Real *u,
+DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Real ud,
                   const Real (&act)[Lay<T, Real>::MPL], const Real (&lce)[Lay<T, Real>::MPL],
                   const Real (&control)[Lay<T, Real>::MPL], int lane, Real *lds, Real h, bool equilibrate,
                   Dyn<T, Real> &D) {
@@ -1002,23 +1017,17 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
     constexpr int ND = LY::ND, NP = LY::NP, NB = T::NB, G = T::G, MPL = LY::MPL;
     static_assert(NB < G && ND <= G, "lane NB writes the ground slot; one lane per dof");
     STAMP_DECL
-    Real x0 = 0;
-    if constexpr (T::TX >= 0) {
-        constexpr int d = T::coord_dof[T::TX];
-        if constexpr (d >= 0) x0 = M.float_origin ? q[d] : Real(0);
-    }
-    D.x0 = x0;
-    if (lane == 0) {
-        Real qf[T::NC], uf[T::NC];
-        fill_coords<T, Real>(M, q, u, qf, uf);
-#pragma unroll
-        for (int c = 0; c < T::NC; ++c) { lds[LY::QF + c] = qf[c]; lds[LY::UF + c] = uf[c]; }
-    }
+    publish_coords<T, Real>(M, SM, lds, lane, qd, ud);
     if (lane < ND) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) lds[LY::SL + 6 * lane + i] = 0;
     }
     wave_sync();
+    Real x0 = 0;
+    if constexpr (T::TX >= 0) {
+        if constexpr (T::coord_dof[T::TX] >= 0) x0 = M.float_origin ? lds[LY::QF + T::TX] : Real(0);
+    }
+    D.x0 = x0;
 
     /* ---- phase 1: lane-parallel kinematics */
     if (lane < NB) kin_local<T, Real>(SM, lds, lane);
@@ -1031,12 +1040,21 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
     if (lane < ND) kin_column<T, Real>(SM, lds, lane);
     if (lane < NB) body_inertia<T, Real>(SM, M, lds, lane);
     wave_sync();
-    /* Plucker columns in registers for the muscle-path lanes */
-    Real Sr[ND][6];
+    /* Plucker columns for the muscle-path lanes: held in registers when they
+     * fit beside the muscle state (planar models), read from LDS otherwise
+     * (the spatial models' 14 columns would spill) */
+    constexpr bool SREG = ND <= 9;
+    Real Sr[SREG ? ND : 1][6];
+    if constexpr (SREG) {
 #pragma unroll
-    for (int d = 0; d < ND; ++d)
+        for (int d = 0; d < ND; ++d)
 #pragma unroll
-        for (int i = 0; i < 6; ++i) Sr[d][i] = lds[LY::S + 6 * d + i];
+            for (int i = 0; i < 6; ++i) Sr[d][i] = lds[LY::S + 6 * d + i];
+    }
+    const auto Sget = [&](int d, int i) -> Real {
+        if constexpr (SREG) return Sr[d][i];
+        else return lds[LY::S + 6 * d + i];
+    };
     STAMP(2);
 
     /* ---- phase 2: lane-parallel force elements */
@@ -1072,7 +1090,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
             if (m < T::NM) {
                 const SMuscle<Real> &mu = SM.mus[m];
                 Real L, dLdq[ND];
-                muscle_path<T, Real>(SM, mu, lds, Sr, L, dLdq);
+                muscle_path<T, Real>(SM, mu, lds, Sget, L, dLdq);
                 STAMP(4);
                 Real a_ = act[j], l_ = lce[j];
                 if (equilibrate) { /* reset: default activation, static fiber equilibrium */
@@ -1195,13 +1213,22 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *
     wave_sync();
     STAMP(8);
 
-    /* ---- phase 4: redundant Cholesky solve in registers */
-    Real A[NP];
+    /* ---- phase 4: Cholesky solve, redundant in every lane's registers (the
+     * shortest dependency chain for these 9x9 / 14x14 systems; a lane-
+     * distributed factorization with one LDS round trip per column measured
+     * 7 % slower per step); lane d keeps q''_d and publishes it for the report */
+    Real A[NP], xs[ND];
 #pragma unroll
     for (int e = 0; e < NP; ++e) A[e] = lds[LY::MP + e];
 #pragma unroll
-    for (int d = 0; d < ND; ++d) D.qdd[d] = lds[LY::RHS + d];
-    D.ok = cholesky_solve<ND, Real>(A, D.qdd);
+    for (int d = 0; d < ND; ++d) xs[d] = lds[LY::RHS + d];
+    D.ok = cholesky_solve<ND, Real>(A, xs);
+    Real x = 0;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) x = lane == d ? xs[d] : x;
+    D.qdd = x;
+    wave_sync();
+    if (lane < ND) lds[LY::RHS + lane] = x;   /* q'' of every dof for the report */
     wave_sync();
     STAMP(9);
 }
@@ -1339,9 +1366,9 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     Dyn<T, Real> D;
 #pragma unroll
     for (int j = 0; j < MPL; ++j) D.ms[j].vN = 0;
-    Real q[ND], u[ND];
-#pragma unroll
-    for (int d = 0; d < ND; ++d) { q[d] = st.q[(size_t)d * N + env]; u[d] = st.u[(size_t)d * N + env]; }
+    /* lane d < ND owns dof d (coordinate value qd, speed ud) */
+    Real qd = 0, ud = 0;
+    if (lane < ND) { qd = st.q[(size_t)lane * N + env]; ud = st.u[(size_t)lane * N + env]; }
     double t = st.t[env];
     int istep = st.istep[env], has_last = st.has_last[env], resets = st.resets[env];
     Real old_px = st.old_px[env];
@@ -1383,16 +1410,17 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
 #pragma unroll
         for (int j = 0; j < MPL; ++j) av[j] = anynan ? Real(0) : raw[j];
         if constexpr ((T::FLAGS & BIOIM_ENV_PD) != 0) {
+            /* PD law on the state at the start of the step (torque_walking_imitation_env2D.py:125-139) */
+            publish_coords<T, Real>(M, SM, lds, lane, qd, ud);
+            wave_sync();
             if (!anynan) {
-                Real qf[T::NC], uf[T::NC];
-                fill_coords<T, Real>(M, q, u, qf, uf);
 #pragma unroll
                 for (int j = 0; j < MPL; ++j) {
                     const int m = lane + j * G;
                     Real xq = 0, xu = 0;
                     sfor<0, NA>([&](auto iI) {
                         constexpr int i = decltype(iI)::value;
-                        if (m == i) { xq = qf[T::pd_coord[i]]; xu = uf[T::pd_vcoord[i]]; }
+                        if (m == i) { xq = lds[LY::QF + T::pd_coord[i]]; xu = lds[LY::UF + T::pd_vcoord[i]]; }
                     });
                     if (m < NA) av[j] = SM.kp[m] * (raw[j] - xq) - SM.kv[m] * xu;
                 }
@@ -1453,11 +1481,11 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         const bool eq = !sub && pending_reset;
         if (eq) {
             int r = clamp_row(reset_row, M.nrows);
-            sfor<0, T::NC>([&](auto cI) {
-                constexpr int c = decltype(cI)::value;
-                constexpr int d = T::coord_dof[c];
-                if constexpr (d >= 0) { q[d] = M.ref_q[r][c]; u[d] = M.ref_u[r][c]; }
-            });
+            if (lane < ND) {
+                const int c = SM.dof_coord[lane];
+                qd = M.ref_q[r][c];
+                ud = M.ref_u[r][c];
+            }
             t = M.ref_time[r];
             istep = M.ref_istep[r];
             has_last = 0;
@@ -1472,12 +1500,11 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             typedef const __attribute__((address_space(4))) DModel<Real> CModel;
             CModel *Mi = (CModel *)Mg;
             asm volatile("" : "+s"(Mi));
-            dynamics<T, Real>(*(const DModel<Real> *)Mi, SM, q, u, act, lce, control, lane, lds, sub ? dt : Real(0),
+            dynamics<T, Real>(*(const DModel<Real> *)Mi, SM, qd, ud, act, lce, control, lane, lds, sub ? dt : Real(0),
                               eq && NM > 0, D);
         }
         if (sub) {
-#pragma unroll
-            for (int d = 0; d < ND; ++d) { u[d] += dt * D.qdd[d]; q[d] += dt * u[d]; }
+            if (lane < ND) { ud += dt * D.qdd; qd += dt * ud; }
             if constexpr (NM > 0) {
 #pragma unroll
                 for (int j = 0; j < MPL; ++j) {
@@ -1530,10 +1557,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                 if (!trans) ob[OL::QPOS + qi] = lds[LY::QF + c];
                 ob[OL::QVEL + c] = lds[LY::UF + c];
                 const int dc = SM.coord_dof[c];
-                Real acc = 0;
-#pragma unroll
-                for (int d = 0; d < ND; ++d) acc = dc == d ? D.qdd[d] : acc;
-                ob[OL::QACC + c] = acc;
+                ob[OL::QACC + c] = dc >= 0 ? lds[LY::RHS + dc] : Real(0);
                 if (tgt && c != T::TX) {
                     const int r1 = clamp_row(istep + 1, M.nrows), ti = c - (T::TX >= 0 && T::TX < c);
                     ob[OL::TGT + ti] = M.ref_q[r1][c];
@@ -1672,8 +1696,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             Real lmax = 0, amax = 0;
 #pragma unroll
             for (int li = 0; li < T::NL; ++li) lmax = fmax(lmax, fabs(lds[LY::LIM + 4 * li]));
-#pragma unroll
-            for (int d = 0; d < ND; ++d) amax = fmax(amax, fabs(D.qdd[d]));
+            amax = group_max<G>(lane < ND ? fabs(D.qdd) : Real(0));
             int d_ = 0;
             if (torso_y < M.torso_y_min) d_ = 1;
             else if (lmax > M.limit_force_max) d_ = 1;
@@ -1682,9 +1705,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             else if constexpr ((T::FLAGS & BIOIM_ENV_DONE_CROSS) != 0) {
                 if (lds[LY::REP + 6 * T::CALCN_R + 2] - lds[LY::REP + 6 * T::CALCN_L + 2] < 0) d_ = 1;
             }
-#pragma unroll
-            for (int d = 0; d < ND; ++d)
-                if (!isfinite(q[d]) || !isfinite(u[d])) d_ = 1;
+            if (group_any<G>(lane < ND && (!isfinite(qd) || !isfinite(ud)))) d_ = 1;
             if (!D.ok) d_ = 1;
             done = d_;
         }
@@ -1721,11 +1742,8 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         st.resets[env] = resets;
     }
     if (lane < ND) {
-        Real qv = q[0], uv = u[0];
-#pragma unroll
-        for (int d = 1; d < ND; ++d) { qv = lane == d ? q[d] : qv; uv = lane == d ? u[d] : uv; }
-        st.q[(size_t)lane * N + env] = qv;
-        st.u[(size_t)lane * N + env] = uv;
+        st.q[(size_t)lane * N + env] = qd;
+        st.u[(size_t)lane * N + env] = ud;
     }
 #pragma unroll
     for (int j = 0; j < MPL; ++j) {
@@ -1927,7 +1945,7 @@ template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, 
     for (int a = 0; a < p.nact && a < SDim<T>::NAD; ++a) { m.kp[a] = (Real)p.kp[a]; m.kv[a] = (Real)p.kv[a]; }
     for (int c = 0; c < p.ncoord; ++c) m.coord_dof[c] = p.coord[c].dof;
     for (int c = 0; c < p.ncoord; ++c)
-        if (p.coord[c].dof >= 0) m.dof_cb[p.coord[c].dof] = p.coord[c].cbody;
+        if (p.coord[c].dof >= 0) { m.dof_cb[p.coord[c].dof] = p.coord[c].cbody; m.dof_coord[p.coord[c].dof] = c; }
     for (int c = 0; c < T::NB; ++c) m.dofmask[c] = T::dofmask[c];
     for (int b = 0; b < T::NOBP; ++b) m.obs_slot[b] = T::obs_bpos[b] >= 0 ? T::obs_bpos[b] : T::NOS;
     for (int b = 0; b < T::NOBV; ++b) m.obs_slot[T::NOBP + b] = T::obs_bvel[b] >= 0 ? T::obs_bvel[b] : T::NOS;
@@ -2010,6 +2028,8 @@ struct bioim_handle {
     uint64_t seed;
     hipStream_t stream;
     bool own_stream;
+    hipStream_t side;     /* private stream: this handle's segment of a concurrent group step */
+    hipEvent_t ev_fork, ev_join;
     void *model;        /* DModel<Real> on device */
     void *smodel;       /* SModel<T, Real> on device (staged into LDS per workgroup) */
     void *state_buf;    /* one allocation for every SoA array */
@@ -2130,6 +2150,7 @@ template <typename Real> int xfer_state(bioim_handle_t *h, double *host, const d
     int nd = h->ndof, nm = h->nmuscle, na = h->nact, H = h->horizon;
     std::vector<char> buf(h->state_bytes);
     HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipStreamSynchronize(h->side));
     HIPCHK(hipMemcpy(buf.data(), h->state_buf, h->state_bytes, hipMemcpyDeviceToHost));
     DState<Real> hs;
     state_layout<Real>(h, buf.data(), &hs);
@@ -2205,6 +2226,12 @@ int bioim_create(const bioim_modelpack_t *pack, int n_envs, int device, int prec
         return fail(BIOIM_E_DEVICE, "bioim_create: stream creation failed");
     }
     h->own_stream = true;
+    if (hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess) {
+        bioim_destroy(h);
+        return fail(BIOIM_E_DEVICE, "bioim_create: stream/event creation failed");
+    }
     int rc = precision == 64 ? alloc_state<double>(h) : alloc_state<float>(h);
     if (rc) { bioim_destroy(h); return rc; }
     *out = h;
@@ -2221,6 +2248,9 @@ int bioim_destroy(bioim_handle_t *h) {
         if (h->precision == 64) delete reinterpret_cast<DState<double> *>(h->dstate);
         else delete reinterpret_cast<DState<float> *>(h->dstate);
     }
+    if (h->side) { hipStreamSynchronize(h->side); hipStreamDestroy(h->side); }
+    if (h->ev_fork) hipEventDestroy(h->ev_fork);
+    if (h->ev_join) hipEventDestroy(h->ev_join);
     if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
     delete h;
     return 0;
@@ -2270,20 +2300,30 @@ int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs
     HIPCHK(hipSetDevice(hs[0]->device));
     const size_t R = hs[0]->precision == 64 ? 8 : 4;
     hipStream_t stream = hs[0]->stream;
-    /* one launch per segment, in order on the first handle's stream.  (A fused two-topology kernel
-     * was tried — workgroups [0, B0) one topology, the rest the other — and dropped: at 4096 envs
-     * each segment already fills the GPU, so it bought only the tail between launches, and its
-     * fp64 build miscompiled the second segment's muscle report) */
+    /* One launch per segment, concurrently: segment 0 on the caller's stream
+     * (hs[0]), segment i > 0 on handle i's private stream, forked from and
+     * joined back into the caller's stream with events.  At 4096 envs per GPU
+     * a mixed 50/50 batch gives each segment half the CUs (one 16-env
+     * workgroup per CU); in order on one stream the halves would run one
+     * after the other.  (A fused two-topology kernel — workgroups [0, B0) one
+     * topology, the rest the other — was tried and dropped: its fp64 build
+     * miscompiled the second segment's muscle report) */
     size_t off = 0;
+    if (nh > 1) HIPCHK(hipEventRecord(hs[0]->ev_fork, stream));
     for (int i = 0; i < nh; ++i) {
         bioim_handle_t *h = hs[i];
         hipStream_t own = h->stream;
-        h->stream = stream;
+        h->stream = i == 0 ? stream : h->side;
+        if (i > 0) HIPCHK(hipStreamWaitEvent(h->side, hs[0]->ev_fork, 0));
         h->ops.launch(h, 0, (const char *)actions + off * h->act_stride * R,
                       obs ? (char *)obs + off * h->obs_stride * R : nullptr,
                       reward ? (char *)reward + off * R : nullptr, done + off,
                       info ? (char *)info + off * h->info_stride * R : nullptr, nullptr, nullptr, 0);
         h->stream = own;
+        if (i > 0) {
+            HIPCHK(hipEventRecord(h->ev_join, h->side));
+            HIPCHK(hipStreamWaitEvent(stream, h->ev_join, 0));
+        }
         off += (size_t)h->n;
     }
     HIPCHK(hipGetLastError());
@@ -2356,6 +2396,7 @@ int bioim_debug_stamps(unsigned long long *out, int reset) {
 int bioim_sync(bioim_handle_t *h) {
     if (!h) return fail(BIOIM_E_ARG, "null handle");
     HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipStreamSynchronize(h->side));
     return 0;
 }
 

@@ -87,8 +87,12 @@ int bioim_set_auto_reset(bioim_handle_t *h, int on);
 int bioim_set_io_strides(bioim_handle_t *h, int act_stride, int obs_stride, int info_stride);
 /* One env step of a mixed batch (BASELINE config C5): handle i
  * owns rows [sum(n_<i), sum(n_<=i)) of the padded buffers (all handles on one
- * device, same precision and strides; auto-reset per handle).  Segments are
- * launched in order on hs[0]'s stream.  Replaces nothing in the reference
+ * device, same precision and strides; auto-reset per handle).  Segment 0 runs
+ * on hs[0]'s stream, the others concurrently on private per-handle streams
+ * forked from and joined back into it (events), so the call is ordered on
+ * hs[0]'s stream like bioim_step.  Later calls on a member handle's own
+ * stream must be ordered after hs[0]'s stream (share one stream, as
+ * VectorEnv does).  Replaces nothing in the reference
  * (one OsimModel per Ray worker); the batch is the RLlib VectorEnv over
  * heterogeneous sub-envs. */
 int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs, void *reward, uint8_t *done,
