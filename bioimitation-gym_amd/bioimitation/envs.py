@@ -142,33 +142,16 @@ class ImitationEnv:
         self._env.close()
 
 
-class MuscleWalkingImitationEnv2D(ImitationEnv):
-    env_id = 'MuscleWalkingImitation2D-v0'
+def _env_class(env_id):
+    """The reference's class name for an env ID (e.g. MuscleWalkingImitation2D-v0 ->
+    MuscleWalkingImitationEnv2D, bioimitation/__init__.py:10-17,89-97)."""
+    stem = env_id[:-len('-v0')]
+    name = stem[:-2] + 'Env' + stem[-2:]
+    return type(name, (ImitationEnv,), {'env_id': env_id, '__doc__': f'{env_id} on the HIP step.'})
 
 
-class TorqueWalkingImitationEnv2D(ImitationEnv):
-    env_id = 'TorqueWalkingImitation2D-v0'
-
-
-class MuscleWalkingImitationEnv3D(ImitationEnv):
-    env_id = 'MuscleWalkingImitation3D-v0'
-
-
-class MuscleRunningImitationEnv3D(ImitationEnv):
-    env_id = 'MuscleRunningImitation3D-v0'
-
-
-class MuscleLockedKneeImitationEnv3D(ImitationEnv):
-    env_id = 'MuscleLockedKneeImitation3D-v0'
-
-
-class MusclePalsyImitationEnv3D(ImitationEnv):
-    env_id = 'MusclePalsyImitation3D-v0'
-
-
-ENV_CLASSES = {c.env_id: c for c in (MuscleWalkingImitationEnv2D, TorqueWalkingImitationEnv2D,
-                                     MuscleWalkingImitationEnv3D, MuscleRunningImitationEnv3D,
-                                     MuscleLockedKneeImitationEnv3D, MusclePalsyImitationEnv3D)}
+ENV_CLASSES = {e: _env_class(e) for e in RECIPES}
+globals().update({c.__name__: c for c in ENV_CLASSES.values()})
 
 
 def make(env_id, config=None, **kw):

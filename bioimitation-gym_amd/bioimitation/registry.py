@@ -16,6 +16,8 @@ SLOW_TWITCH_3D = [0.499, 0.55, 0.5, 0.484, 0.546, 0.759, 0.721, 0.484, 0.546, 0.
 PD_COORDS_2D = ['pelvis_tilt', 'hip_flexion_r', 'knee_angle_r', 'ankle_angle_r',
                 'hip_flexion_l', 'knee_angle_l', 'ankle_angle_l']
 
+_PD_2D = dict(pd=True, pd_coords=PD_COORDS_2D, kp=[100, 100, 100, 50, 100, 100, 50], kv=[5, 5, 5, 2, 5, 5, 2])
+
 # env id -> (model file relative to the reference data dir, transforms, spec kwargs)
 RECIPES = {
     # torque_walking_imitation_env2D.py:18-366 (PD :117-149, done :249-277, reward :279-366)
@@ -23,8 +25,7 @@ RECIPES = {
         model='2D/scale/model_scaled.osim', transforms=('predictive', 'torque'),
         reference='2D/walking_reference_data',
         spec=dict(muscle=False, three_d=False, cycle=132, n_episode=264, reset_hi=132,
-                  acc_max=1e5, pd=True, pd_coords=PD_COORDS_2D,
-                  kp=[100, 100, 100, 50, 100, 100, 50], kv=[5, 5, 5, 2, 5, 5, 2])),
+                  acc_max=1e5, **_PD_2D)),
     # muscle_walking_imitation_env2D.py:17-403 (done :237-265, reward :267-358, COT :360-403)
     'MuscleWalkingImitation2D-v0': dict(
         model='2D/scale/model_scaled.osim', transforms=('predictive',),
@@ -66,6 +67,69 @@ RECIPES.update({
         model='02905/02905_PRE/scale/model_predictive.osim', transforms=(),
         reference='02905/walking_reference_data', ik=_IK_PALSY,
         spec=dict(cycle=50, n_episode='rows-2', reset_hi=50, raw_action=True, **_SPEC_3D)),
+})
+
+# torque_*_imitation_env3D.py:128-139: PD on x = coordinate_pos (pelvis translations deleted)[0:11] and
+# v = coordinate_vel (all 17)[[0, 4, 5, 6, 8, 8, 9, 10, 11, 12, 13]] — the speed indices do not match the
+# position ones (pelvis_ty/tz, hip_rotation_r twice); reproduced as written
+PD_COORDS_3D = ['pelvis_tilt', 'pelvis_list', 'pelvis_rotation', 'hip_flexion_r', 'hip_adduction_r',
+                'hip_rotation_r', 'knee_angle_r', 'ankle_angle_r', 'hip_flexion_l', 'hip_adduction_l', 'hip_rotation_l']
+PD_VCOORDS_3D = ['pelvis_tilt', 'pelvis_ty', 'pelvis_tz', 'hip_flexion_r', 'hip_rotation_r', 'hip_rotation_r',
+                 'knee_angle_r', 'ankle_angle_r', 'hip_flexion_l', 'hip_adduction_l', 'hip_rotation_l']
+_PD_3D = dict(pd=True, pd_coords=PD_COORDS_3D, pd_vcoords=PD_VCOORDS_3D,
+              kp=[100, 100, 100, 100, 100, 50, 100, 100, 100, 100, 50], kv=[5, 5, 5, 5, 5, 2, 5, 5, 5, 5, 2])
+# limit force 1e4, |qdd| 1e6 (the variants' is_done), exp(-|da|) action reward
+_LOOSE = dict(limit_force_max=1e4, acc_max=1e6)
+_IK_2D = '3D/inverse_kinematics/task_InverseKinematics.mot'
+
+RECIPES.update({
+    # muscle_locked_knee_imitation_env2D.py: never calls its convert_model_to_prosthetic (:102, no call
+    # site), so the simulated model is the 2D muscle model; cycle 132, N = 2*cycle (:73-77), reset
+    # randint(0, N/2) (:167), done limit 1e4 / qdd 1e6 (:281-283)
+    'MuscleLockedKneeImitation2D-v0': dict(
+        model='2D/scale/model_scaled.osim', transforms=('predictive',),
+        reference='2D/walking_reference_data',
+        spec=dict(muscle=True, three_d=False, cycle=132, n_episode=264, reset_hi=132, slow_twitch=SLOW_TWITCH_2D,
+                  raw_action=True, **_LOOSE)),   # physics gets the raw action (:154)
+    # muscle_running_imitation_env2D.py: cycle 70 (:176), N = rows - 2 (:73-75), reset randint(0, N/2)
+    # (:142).  The reference never sets self.w_effort (:30-31) and raises AttributeError in get_reward
+    # (:341); here w_effort = r_weights[1] as in every other env.  running_reference_data/ is absent:
+    # the 2D walking tables are used.
+    'MuscleRunningImitation2D-v0': dict(
+        model='2D/scale/model_scaled.osim', transforms=('predictive',),
+        reference='2D/walking_reference_data',
+        spec=dict(muscle=True, three_d=False, cycle=70, n_episode='rows-2', reset_hi='N/2',
+                  slow_twitch=SLOW_TWITCH_2D, raw_action=True, **_LOOSE)),   # raw action to physics (:129)
+    # torque_running_imitation_env2D.py: cycle 70 (:195), N = rows - 2 (:76-78), reset N/2 (:161)
+    'TorqueRunningImitation2D-v0': dict(
+        model='2D/scale/model_scaled.osim', transforms=('predictive', 'torque'),
+        reference='2D/walking_reference_data',
+        spec=dict(muscle=False, three_d=False, cycle=70, n_episode='rows-2', reset_hi='N/2', **_PD_2D, **_LOOSE)),
+    # torque_locked_knee_imitation_env2D.py: torque model, then knee_l/ankle_l locked (:61-62, :105-123);
+    # their actuators stay (no effect on a locked coordinate); cycle 132, N = 2*cycle, reset N/2
+    'TorqueLockedKneeImitation2D-v0': dict(
+        model='2D/scale/model_scaled.osim', transforms=('predictive', 'torque', 'prosthetic'),
+        reference='2D/walking_reference_data',
+        spec=dict(muscle=False, three_d=False, cycle=132, n_episode=264, reset_hi=132, **_PD_2D, **_LOOSE)),
+    # torque_walking_imitation_env3D.py: cycle 132 (:75), N = 2*cycle (:79), reset N/2 (:162),
+    # effort |a|/(max_actuation*11^2) (:353), exp(-|da|) (:355), feet in the reward (:357)
+    'TorqueWalkingImitation3D-v0': dict(
+        model='3D/scale/model_scaled.osim', transforms=('predictive', 'torque'),
+        reference='3D/walking_reference_data', ik=_IK_3D,
+        spec=dict(muscle=False, three_d=True, cycle=132, n_episode=264, reset_hi=132, reward_feet=True,
+                  done_cross=True, **_PD_3D, **_LOOSE)),
+    # torque_running_imitation_env3D.py: cycle 70 (:195), N = rows - 2 (:76-78), reset N/2 (:161)
+    'TorqueRunningImitation3D-v0': dict(
+        model='3D/scale/model_scaled.osim', transforms=('predictive', 'torque'),
+        reference='3D/walking_reference_data', ik=_IK_3D,
+        spec=dict(muscle=False, three_d=True, cycle=70, n_episode='rows-2', reset_hi='N/2', reward_feet=True,
+                  done_cross=True, **_PD_3D, **_LOOSE)),
+    # torque_locked_knee_imitation_env3D.py: torque model, then prosthetic (:61-62); cycle 132, N = 2*cycle
+    'TorqueLockedKneeImitation3D-v0': dict(
+        model='3D/scale/model_scaled.osim', transforms=('predictive', 'torque', 'prosthetic'),
+        reference='3D/walking_reference_data', ik=_IK_3D,
+        spec=dict(muscle=False, three_d=True, cycle=132, n_episode=264, reset_hi=132, reward_feet=True,
+                  done_cross=True, **_PD_3D, **_LOOSE)),
 })
 
 # mixed-topology batches (BASELINE.json config C5, bench.py --mixed): the prosthetic (12 dof,

@@ -102,7 +102,8 @@ for name, rel in [('bioimitation', 'bioimitation'), ('bioimitation.imitation_env
                   ('bioimitation.imitation_envs.envs.muscle.planar', 'bioimitation/imitation_envs/envs/muscle/planar'),
                   ('bioimitation.imitation_envs.envs.muscle.spatial', 'bioimitation/imitation_envs/envs/muscle/spatial'),
                   ('bioimitation.imitation_envs.envs.torque', 'bioimitation/imitation_envs/envs/torque'),
-                  ('bioimitation.imitation_envs.envs.torque.planar', 'bioimitation/imitation_envs/envs/torque/planar')]:
+                  ('bioimitation.imitation_envs.envs.torque.planar', 'bioimitation/imitation_envs/envs/torque/planar'),
+                  ('bioimitation.imitation_envs.envs.torque.spatial', 'bioimitation/imitation_envs/envs/torque/spatial')]:
     m = types.ModuleType(name)
     m.__path__ = [os.path.join(REF, rel)]
     sys.modules[name] = m
@@ -465,6 +466,53 @@ def main():
         e1['config'] = e2['config'] = repr(config)
         e2['chained'] = 1
         eps += [e1, e2]
+        out[env_id] = eps
+
+    # ---------------- remaining variants (muscle/torque locked-knee, running, torque 3D)
+    rng2 = np.random.Generator(np.random.PCG64(7))
+    variants = [('MuscleLockedKneeImitation2D-v0', 'muscle.planar.muscle_locked_knee_imitation_env2D',
+                 'MuscleLockedKneeImitationEnv2D'),
+                ('MuscleRunningImitation2D-v0', 'muscle.planar.muscle_running_imitation_env2D',
+                 'MuscleRunningImitationEnv2D'),
+                ('TorqueRunningImitation2D-v0', 'torque.planar.torque_running_imitation_env2D',
+                 'TorqueRunningImitationEnv2D'),
+                ('TorqueLockedKneeImitation2D-v0', 'torque.planar.torque_locked_knee_imitation_env2D',
+                 'TorqueLockedKneeImitationEnv2D'),
+                ('TorqueWalkingImitation3D-v0', 'torque.spatial.torque_walking_imitation_env3D',
+                 'TorqueWalkingImitationEnv3D'),
+                ('TorqueRunningImitation3D-v0', 'torque.spatial.torque_running_imitation_env3D',
+                 'TorqueRunningImitationEnv3D'),
+                ('TorqueLockedKneeImitation3D-v0', 'torque.spatial.torque_locked_knee_imitation_env3D',
+                 'TorqueLockedKneeImitationEnv3D')]
+    for j, (env_id, modfile, cls) in enumerate(variants):
+        mod = 'bioimitation.imitation_envs.envs.' + modfile
+        hi = registry.load_pack(env_id).reset_hi
+        torque = env_id.startswith('Torque')
+        eps = []
+        for k, (index, T, nan_at, cfg) in enumerate([(29, 14, (), {}), (None, 30, (5,), {}),
+                                                     (0, 10, (), {'mode': 'test'}),
+                                                     (min(hi, 43), 20, (), {'horizon': 3, 'use_GRF': False})]):
+            config = dict(DEFAULT_CFG, **cfg)
+            env, pk = make_env(env_id, mod, cls, config)
+            if env_id == 'MuscleRunningImitation2D-v0':
+                env.w_effort = config['r_weights'][1]   # never set by the reference (its get_reward raises)
+            seed = 5000 + 10 * j + k if index is None else seed_for_index(index, hi)
+            if torque:
+                noise = rng2.normal(0.0, 0.05, size=(T, pk.nact))
+                pdc = [CURRENT['names']['coords'][pk.pd_coord[i]] for i in range(pk.nact)]
+
+                def act(t, e, noise=noise, pdc=pdc):
+                    row = e.q_d.iloc[min(e.osim_model.istep + 1, len(e.q_d) - 1)]
+                    return np.array([row[c] for c in pdc]) + noise[t]
+            else:
+                acts = rng2.uniform(0.0, 1.0, size=(T, pk.nact))
+
+                def act(t, e, acts=acts):
+                    return acts[t].copy()
+            ep = run_episode(env, pk, seed, T, act, nan_at)
+            ep['config'] = repr(config)
+            eps.append(ep)
+            print(env_id, 'episode', k, 'index', ep['index'], 'steps', len(ep['reward']), 'done', ep['done'][-1])
         out[env_id] = eps
 
     for env_id, eps in out.items():

@@ -10,9 +10,9 @@ import pytest
 
 from bioimitation.registry import load_pack
 
-GOLDEN = {e: f'tests/golden/{e}.npz' for e in (
-    'MuscleWalkingImitation2D-v0', 'TorqueWalkingImitation2D-v0', 'MuscleWalkingImitation3D-v0',
-    'MuscleRunningImitation3D-v0', 'MuscleLockedKneeImitation3D-v0', 'MusclePalsyImitation3D-v0')}
+from bioimitation.registry import RECIPES
+
+GOLDEN = {e: f'tests/golden/{e}.npz' for e in RECIPES}     # every built env ID has fixtures
 
 
 def episodes(path):

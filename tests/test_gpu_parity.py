@@ -6,13 +6,12 @@ Tolerances (north_star: obs/reward within 1e-4 rel of the fp64 reference):
     differ; observed 1.6e-9 over 2D and 3D);
   - precision 32 (fast mode), per-step re-synced (the oracle state is loaded
     into the GPU before every step): reward and info within 1e-4 (observed
-    < 4e-6); state-like observation columns (phase, q, targets, body
-    positions/velocities, activations, fiber lengths) within 5e-4 of
-    max(|x|, 1); rate-like columns that are roots of ill-conditioned
-    equations within 1e-2: coordinate speeds (one substep of q''), fiber
-    velocities (the damped-equilibrium root), contact forces (Stribeck
-    friction near zero slip); observed worst 5.5e-3 (3D LockedKnee glut_max
-    fiber velocity).  The generalized accelerations (coordinate_acc block)
+    < 2.1e-5); state-like observation columns (phase, q, targets, body
+    positions, activations, fiber lengths) within 5e-4 of max(|x|, 1);
+    rate-like columns within 1e-2: coordinate and body speeds (one substep
+    of q''), fiber velocities (the damped-equilibrium root), contact forces
+    (Stribeck friction near zero slip); observed worst 5.5e-3 (3D LockedKnee
+    glut_max fiber velocity).  The generalized accelerations (coordinate_acc block)
     are a difference of large opposing muscle/contact/gravity torques divided
     through ~1e-2 kg m^2 effective inertias; near contact onset the linearly
     implicit contact terms amplify fp32 rounding, so fp32 resolves q'' only to
@@ -27,8 +26,9 @@ from conftest import gpu_available
 
 pytestmark = pytest.mark.gpu
 
-ENV_IDS = ['MuscleWalkingImitation2D-v0', 'TorqueWalkingImitation2D-v0', 'MuscleWalkingImitation3D-v0',
-           'MuscleRunningImitation3D-v0', 'MuscleLockedKneeImitation3D-v0', 'MusclePalsyImitation3D-v0']
+from bioimitation.registry import RECIPES
+
+ENV_IDS = list(RECIPES)          # every built env ID (13)
 QUIRK_ROWS = [0, 29, 58, 59, 116, 117, 132]
 
 
@@ -148,8 +148,8 @@ def test_step_parity_fp32_resynced(env_id):
     col_err = np.zeros(len(other))
     from bioimitation.obslayout import column_names, load_names
     names = column_names(pk, load_names(env_id))
-    rate = np.array([names[c].startswith(('coordinate_vel', 'contact_forces')) or names[c].endswith('fiber_velocity')
-                     for c in other])
+    rate = np.array([names[c].startswith(('coordinate_vel', 'body_vel', 'contact_forces')) or
+                     names[c].endswith('fiber_velocity') for c in other])
     for t in range(T):
         env.set_state(np.stack([orc.get_state(bufs, i) for i in range(n)]))
         st = np.array([orc.get_state(bufs, i)[1] for i in range(n)]).astype(int)

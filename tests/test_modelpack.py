@@ -63,6 +63,31 @@ def test_model_facts_3d(env_id, ndof, ncbody, nm, obs, mass, cycle, n_episode, r
     assert locked == ([8, 13, 16] if ndof == 14 else [8, 13, 14, 15, 16])
 
 
+# the remaining variants
+@pytest.mark.parametrize('env_id,ncoord,ndof,ncbody,nm,nact,obs,info', [
+    ('MuscleLockedKneeImitation2D-v0', 9, 9, 7, 14, 14, 138, 5),
+    ('MuscleRunningImitation2D-v0', 9, 9, 7, 14, 14, 138, 5),
+    ('TorqueRunningImitation2D-v0', 9, 9, 7, 0, 7, 96, 4),
+    ('TorqueLockedKneeImitation2D-v0', 9, 7, 5, 0, 7, 96, 4),
+    ('TorqueWalkingImitation3D-v0', 17, 14, 7, 0, 11, 135, 4),
+    ('TorqueRunningImitation3D-v0', 17, 14, 7, 0, 11, 135, 4),
+    ('TorqueLockedKneeImitation3D-v0', 17, 12, 5, 0, 11, 135, 4)])
+def test_model_facts_variants(env_id, ncoord, ndof, ncbody, nm, nact, obs, info):
+    pk = load_pack(env_id)
+    assert (pk.ncoord, pk.ndof, pk.ncbody, pk.nmuscle, pk.nact, pk.obs_dim, pk.info_dim) == \
+        (ncoord, ndof, ncbody, nm, nact, obs, info)
+    assert (pk.limit_force_max, pk.acc_max) == (1e4, 1e6)
+    if env_id.startswith('Torque'):
+        assert pk.env_flags & P.ENV_PD and pk.ncoordact == nact
+        # the prosthetic keeps its knee_l/ankle_l actuators on locked coordinates (no dof)
+        assert sum(pk.coordact[a].dof < 0 for a in range(nact)) == (2 if 'LockedKnee' in env_id else 0)
+    if env_id.endswith('3D-v0') and env_id.startswith('Torque'):
+        # torque_walking_imitation_env3D.py:130-131: q indices 0..10 of the translation-free list,
+        # q' indices [0, 4, 5, 6, 8, 8, 9, 10, 11, 12, 13] of the full list
+        assert [pk.pd_coord[i] for i in range(11)] == [0, 1, 2, 6, 7, 8, 9, 10, 11, 12, 13]
+        assert [pk.pd_vcoord[i] for i in range(11)] == [0, 4, 5, 6, 8, 8, 9, 10, 11, 12, 13]
+
+
 def test_config_patching():
     base = load_pack('MuscleWalkingImitation2D-v0')
     pk = load_pack('MuscleWalkingImitation2D-v0', {'use_target_obs': False, 'use_GRF': False, 'horizon': 3,
@@ -73,7 +98,7 @@ def test_config_patching():
     with pytest.raises(ValueError):
         load_pack('MuscleWalkingImitation2D-v0', {'horizon': 99})
     with pytest.raises(NotImplementedError):
-        load_pack('MuscleJumpingImitation2D-v0')
+        load_pack('MuscleJumpingImitation3D-v0')
 
 
 def test_spline_interpolates_knots_and_is_c2():
