@@ -22,7 +22,7 @@ import random
 
 import numpy as np
 
-from .registry import REGISTERED_IDS, RECIPES, load_pack
+from .registry import NOT_BUILT, RECIPES, load_pack
 
 DEFAULT_CONFIG = {  # configs/env_default.py keys the envs read
     'mode': 'train', 'visualize': False, 'max_actuation': 200.0, 'log': False,
@@ -157,8 +157,8 @@ globals().update({c.__name__: c for c in ENV_CLASSES.values()})
 def make(env_id, config=None, **kw):
     """Construct the env class registered under ``env_id``."""
     if env_id not in ENV_CLASSES:
-        if env_id in REGISTERED_IDS:
-            raise NotImplementedError(f'{env_id} is registered by the reference but not built yet')
+        if env_id in NOT_BUILT:
+            raise NotImplementedError(f'{env_id}: {NOT_BUILT[env_id]}')
         raise KeyError(env_id)
     return ENV_CLASSES[env_id](config, **kw)
 

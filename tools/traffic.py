@@ -9,7 +9,7 @@ uncalibrated width, so the raw value is recorded next to the doubled one and
 bench.py reports the raw FETCH + WRITE sum (a lower bound on bytes moved).
 The reset dispatch (first, much shorter) is excluded.
 
-    python tools/traffic.py <prof_dir> <env_id> <precision> <envs>
+    python tools/traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <env_id> <precision> <envs>
 """
 import csv
 import json
@@ -25,9 +25,10 @@ def per_launch(path):
 
 
 def main():
-    d, env_id, prec, n = sys.argv[1:5]
-    fetch = per_launch(os.path.join(d, 'fetch', 'fetch_counter_collection.csv'))
-    write = per_launch(os.path.join(d, 'write', 'write_counter_collection.csv'))
+    fcsv, wcsv, env_id, prec, n = sys.argv[1:6]
+    fetch = per_launch(fcsv)
+    write = per_launch(wcsv)
+    d = os.path.dirname(os.path.dirname(fcsv))
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles', 'traffic.json')
     db = json.load(open(out)) if os.path.exists(out) else {}
     db[f'{env_id}/fp{prec}/{n}'] = {'bytes': fetch + write, 'fetch_bytes_raw': fetch, 'fetch_bytes_x2': 2 * fetch,
