@@ -6,14 +6,15 @@ UtkarshMishra04/bioimitation-gym), ``Env(config)`` classes with
 """
 from .registry import REGISTERED_IDS, RECIPES, env_spec, load_pack  # noqa: F401
 
-__all__ = ['REGISTERED_IDS', 'RECIPES', 'env_spec', 'load_pack', 'VectorEnv', 'make']
+__all__ = ['REGISTERED_IDS', 'RECIPES', 'env_spec', 'load_pack', 'VectorEnv', 'MixedVectorEnv', 'make',
+           'RLlibVectorEnv', 'GymVectorEnv', 'MeanStdFilter']
+
+_LAZY = {'VectorEnv': 'vector_env', 'MixedVectorEnv': 'vector_env', 'make': 'envs', 'RLlibVectorEnv': 'adapters',
+         'GymVectorEnv': 'adapters', 'MeanStdFilter': 'adapters'}
 
 
 def __getattr__(name):
-    if name == 'VectorEnv':
-        from .vector_env import VectorEnv
-        return VectorEnv
-    if name == 'make':
-        from .envs import make
-        return make
+    if name in _LAZY:
+        import importlib
+        return getattr(importlib.import_module('.' + _LAZY[name], __name__), name)
     raise AttributeError(name)

@@ -1,0 +1,170 @@
+"""Consumer adapters around :class:`~bioimitation.vector_env.VectorEnv`
+(SURVEY.md 8f rank 3): the step on either side of the HIP path.
+
+The reference trains with RLlib PPO (``configs/train_default.py``:
+``observation_filter = "MeanStdFilter"``, one env per rollout worker,
+``register_env(ID, lambda config: Env(config))`` in ``bioimitation/__init__.py``)
+or with a jaxrl SAC loop (``tests/sample_baselines_training.py:69-91``).
+Neither ray nor gym is importable here, so the adapters are duck-typed:
+
+- :class:`RLlibVectorEnv` — RLlib's ``VectorEnv`` protocol (``vector_reset``,
+  ``reset_at``, ``vector_step``, ``get_sub_environments``): N envs of one ID
+  stepped by one kernel launch; RLlib itself calls ``reset_at`` on done, so
+  in-kernel auto-reset is off.
+- :class:`GymVectorEnv` — gym's vector-env convention (batched ``reset`` /
+  ``step``, finished envs reset automatically and report their reset
+  observation): in-kernel auto-reset on.
+- :class:`MeanStdFilter` — RLlib's ``MeanStdFilter`` (demean, destd,
+  clip 10) as a running mean/variance kept on the GPU and updated from whole
+  batches, so normalised observations never leave the device.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .vector_env import VectorEnv
+
+
+class MeanStdFilter:
+    """Running observation normaliser on the device.
+
+    Statistics follow RLlib's ``RunningStat`` (Welford: mean, sum of squared
+    deviations ``S``, count ``n``; ``var = S / (n - 1)`` for n > 1, ``mean**2``
+    for n == 1) and the filter's output is ``clip((x - mean) / (std + 1e-8),
+    -clip, clip)``.  A batch is pushed with Chan's parallel update, which
+    equals pushing its rows one by one up to rounding; unlike RLlib, every
+    row of a batch is normalised with the statistics after the whole batch."""
+
+    def __init__(self, shape, demean: bool = True, destd: bool = True, clip: float = 10.0, device=None,
+                 dtype=None):
+        import torch
+        self.shape = tuple(shape) if not isinstance(shape, int) else (shape,)
+        self.demean, self.destd, self.clip = demean, destd, clip
+        self.n = 0
+        self.mean = torch.zeros(self.shape, dtype=dtype or torch.float64, device=device)
+        self.S = torch.zeros_like(self.mean)
+
+    @property
+    def var(self):
+        import torch
+        if self.n > 1:
+            return self.S / (self.n - 1)
+        return torch.square(self.mean)
+
+    @property
+    def std(self):
+        import torch
+        return torch.sqrt(self.var)
+
+    def push(self, batch):
+        """Add a batch of observations (B, *shape)."""
+        import torch
+        x = batch.reshape((-1,) + self.shape).to(self.mean.dtype)
+        b = x.shape[0]
+        if b == 0:
+            return
+        bm = x.mean(0)
+        bS = torch.square(x - bm).sum(0)
+        n = self.n + b
+        delta = bm - self.mean
+        self.mean = self.mean + delta * (b / n)
+        self.S = self.S + bS + torch.square(delta) * (self.n * b / n)
+        self.n = n
+
+    def __call__(self, batch, update: bool = True):
+        import torch
+        if update:
+            self.push(batch)
+        x = batch.to(self.mean.dtype)
+        if self.demean:
+            x = x - self.mean
+        if self.destd:
+            x = x / (self.std + 1e-8)
+        if self.clip:
+            x = torch.clamp(x, -self.clip, self.clip)
+        return x.to(batch.dtype)
+
+    def state_dict(self):
+        return {'n': self.n, 'mean': self.mean.clone(), 'S': self.S.clone()}
+
+    def load_state_dict(self, d):
+        self.n, self.mean, self.S = int(d['n']), d['mean'].clone(), d['S'].clone()
+
+
+def _spaces(env: VectorEnv):
+    from .envs import _box
+    pk = env.pack
+    if pk.nmuscle:
+        lo, hi = [0.0] * pk.nact, [1.0] * pk.nact
+    else:
+        lo = [pk.coordact[a].min_control for a in range(pk.nact)]
+        hi = [pk.coordact[a].max_control for a in range(pk.nact)]
+    return _box([-np.inf] * env.obs_dim, [np.inf] * env.obs_dim), _box(lo, hi)
+
+
+class RLlibVectorEnv:
+    """RLlib ``VectorEnv`` protocol over one batched HIP env (numpy I/O, as
+    RLlib's sampler expects).  ``reset_at`` resets one env on the device
+    (``random.randint``-equivalent row drawn by the kernel's counter RNG)."""
+
+    def __init__(self, env_id: str, num_envs: int, config: dict = None, device: int = 0, precision: int = 64,
+                 seed: int = 0, env_offset: int = 0):
+        self.env = VectorEnv(env_id, num_envs, config=config, device=device, precision=precision, seed=seed,
+                             auto_reset=False, env_offset=env_offset)
+        self.num_envs = num_envs
+        self.observation_space, self.action_space = _spaces(self.env)
+
+    def vector_reset(self):
+        return list(self.env.reset().double().cpu().numpy())
+
+    def reset_at(self, index: int):
+        obs = self.env.reset(env_ids=[int(index)])
+        return obs[int(index)].double().cpu().numpy()
+
+    def vector_step(self, actions):
+        import torch
+        a = torch.as_tensor(np.asarray(actions, dtype=np.float64), device=self.env.device)
+        obs, rew, done, info = self.env.step(a)
+        obs, rew, done, info = (t.double().cpu().numpy() for t in (obs, rew, done, info))
+        infos = [{'all_rewards': list(map(float, r))} for r in info]
+        return list(obs), list(map(float, rew)), list(map(bool, done)), infos
+
+    def get_sub_environments(self):
+        return []
+
+    get_unwrapped = get_sub_environments
+
+    def try_render_at(self, index=None):
+        return None
+
+    def close(self):
+        self.env.close()
+
+
+class GymVectorEnv:
+    """gym vector-env convention on the device: ``reset() -> obs (N, O)``,
+    ``step(actions) -> (obs, rewards, dones, infos)`` with finished envs reset
+    in the same kernel launch (their obs row is the post-reset observation).
+    ``normalize=True`` applies a device :class:`MeanStdFilter` to the
+    observations (RLlib's ``observation_filter``)."""
+
+    def __init__(self, env_id: str, num_envs: int, config: dict = None, device: int = 0, precision: int = 64,
+                 seed: int = 0, env_offset: int = 0, normalize: bool = False):
+        self.env = VectorEnv(env_id, num_envs, config=config, device=device, precision=precision, seed=seed,
+                             auto_reset=True, env_offset=env_offset)
+        self.num_envs = num_envs
+        self.single_observation_space, self.single_action_space = _spaces(self.env)
+        self.filter = MeanStdFilter(self.env.obs_dim, device=self.env.device) if normalize else None
+
+    def _obs(self, obs):
+        return self.filter(obs) if self.filter is not None else obs
+
+    def reset(self):
+        return self._obs(self.env.reset())
+
+    def step(self, actions):
+        obs, rew, done, info = self.env.step(actions)
+        return self._obs(obs), rew, done.bool(), {'all_rewards': info}
+
+    def close(self):
+        self.env.close()
