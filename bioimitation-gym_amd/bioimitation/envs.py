@@ -77,13 +77,17 @@ class ImitationEnv:
     def __init__(self, config=None, device=0, precision=64, seed=0):
         cfg = dict(DEFAULT_CONFIG)
         cfg.update(config or {})
-        if cfg.get('apply_perturbations'):
-            raise NotImplementedError('apply_perturbations (torso PrescribedForce) is not part of the HIP step')
         from .vector_env import VectorEnv
         self.config = cfg
         self.test = cfg.get('mode') == 'test'
-        self._env = VectorEnv(self.env_id, 1, config=cfg, device=device, precision=precision, seed=seed,
-                              auto_reset=False)
+        self._env = VectorEnv(self.env_id, 1, config=dict(cfg, apply_perturbations=False), device=device,
+                              precision=precision, seed=seed, auto_reset=False)
+        if cfg.get('apply_perturbations'):
+            # one schedule per construction from NumPy's global RNG, like the
+            # reference (muscle_walking_imitation_env2D.py:83-100)
+            from .perturb import reference_points
+            x, y = reference_points(self.env_id)
+            self._env.set_perturbation(x, y[None, :])
         pk = self._env.pack
         self.N = pk.n_episode
         self.cycle = pk.cycle

@@ -52,6 +52,31 @@ class VectorEnv:
         self.reward = torch.zeros(n, dtype=self.dtype, device=self.device)
         self.done = torch.zeros(n, dtype=torch.uint8, device=self.device)
         self.info = torch.zeros((n, self.info_dim), dtype=self.dtype, device=self.device)
+        self.perturbation = None
+        if (config or {}).get('apply_perturbations'):
+            from .perturb import batch_points
+            self.set_perturbation(*batch_points(env_id, n, seed=(config or {}).get('perturbation_seed', seed),
+                                                env_offset=env_offset))
+
+    def set_perturbation(self, x, y, body='torso'):
+        """apply_perturbations (muscle_walking_imitation_env2D.py:83-100): the
+        reference's PiecewiseConstantFunction points ``x`` [n] (shared) and
+        ``y`` [num_envs][n] (N) of the ground-x force on ``body``'s origin;
+        ``x=None`` removes it.  Converted to the device's zero-order-hold
+        table by :func:`bioimitation.perturb.zoh_table`."""
+        from .obslayout import load_names
+        from .perturb import os_body_index, zoh_table
+        if x is None:
+            _lib.check(self._L.bioim_set_perturbation(self._h, -1, 0, None, None))
+            self.perturbation = None
+            return
+        xt, yt = zoh_table(x, y)
+        yt = np.ascontiguousarray(np.broadcast_to(yt, (self.num_envs, len(xt))), dtype=np.float64)
+        ob = os_body_index(load_names(self.env_id), body)
+        dp = C.POINTER(C.c_double)
+        xt = np.ascontiguousarray(xt)
+        _lib.check(self._L.bioim_set_perturbation(self._h, ob, len(xt), xt.ctypes.data_as(dp), yt.ctypes.data_as(dp)))
+        self.perturbation = (np.asarray(x, dtype=np.float64), yt)
 
     @staticmethod
     def _ptr(t):

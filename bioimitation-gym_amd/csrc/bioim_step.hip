@@ -357,6 +357,10 @@ template <class T, typename Real> struct Lay {
     static constexpr int SIZE = ((U + USZ + 1) / 2) * 2;
 };
 
+/* apply_perturbations kernels only: per env 5 doubles after all env regions
+ * (call time base, substep length, cursor segment [lo, hi), its force) */
+constexpr int PERT_SLOT = 5;
+
 DEV void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1003,16 +1007,43 @@ template <class T, typename Real> struct Dyn {
     bool ok;
 };
 
+/* apply_perturbations table (see LaunchArgs) as seen by one env */
+template <typename Real> struct PertArgs {
+    const double *x;
+    const Real *y;   /* [n][N] */
+    int n, ob, env, N;
+};
+
+/* Force of the env's zero-order-hold table at the call time t0 + k*dt (the
+ * slot's base and step, written by lane 0 before the call); the segment
+ * cursor [lo, hi) and its value live in the slot, so a binary search over
+ * the table runs only when the time leaves the segment. */
+template <typename Real>
+DEV Real pert_force(const PertArgs<Real> &P, double *sl, int k) {
+    const double tc = sl[0] + (double)k * sl[1];
+    if (!(tc >= sl[2] && tc < sl[3])) {
+        int lo = -1, hi = P.n;               /* x[lo] <= tc < x[hi] */
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (P.x[mid] <= tc) lo = mid; else hi = mid;
+        }
+        sl[2] = lo >= 0 ? P.x[lo] : -INFINITY;
+        sl[3] = hi < P.n ? P.x[hi] : INFINITY;
+        sl[4] = (double)P.y[(size_t)(lo >= 0 ? lo : 0) * P.N + P.env];
+    }
+    return (Real)sl[4];
+}
+
 /* Forward dynamics at (q, u, this lane's muscle states) with held controls.
  * Lane d < ND owns dof d (qd, ud in, D.qdd out); lane's j-th muscle is
  * m = lane + j*G.  h > 0: increment of the linearly-implicit substep;
  * h == 0: the true accelerations (realize).  Leaves coordinates, frames,
  * contact wrenches, limit forces and q'' (RHS slots) published in LDS. */
-template <class T, typename Real>
+template <class T, typename Real, bool PERT>
 DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Real ud,
                   const Real (&act)[Lay<T, Real>::MPL], const Real (&lce)[Lay<T, Real>::MPL],
                   const Real (&control)[Lay<T, Real>::MPL], int lane, Real *lds, Real h, bool equilibrate,
-                  Dyn<T, Real> &D) {
+                  const PertArgs<Real> &P, double *pslot, int pk, Dyn<T, Real> &D) {
     using LY = Lay<T, Real>;
     constexpr int ND = LY::ND, NP = LY::NP, NB = T::NB, G = T::G, MPL = LY::MPL;
     static_assert(NB < G && ND <= G, "lane NB writes the ground slot; one lane per dof");
@@ -1038,7 +1069,21 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     wave_sync();
     STAMP(1);
     if (lane < ND) kin_column<T, Real>(SM, lds, lane);
-    if (lane < NB) body_inertia<T, Real>(SM, M, lds, lane);
+    if (lane < NB) {
+        body_inertia<T, Real>(SM, M, lds, lane);
+        /* apply_perturbations: ground-frame force (fx, 0, 0) at the origin of
+         * OpenSim body P.ob (the torso), muscle_walking_imitation_env2D.py:83-100 */
+        if (PERT && lane == SM.os_cb[P.ob]) {
+            const Real fpx = pert_force<Real>(P, pslot, pk);
+            const Real *kb = lds + LY::KB + 18 * lane;
+            Real p[3];
+            mv3(kb, SM.os_p[P.ob], p);
+            Real *wb = lds + LY::WB + 6 * lane;
+            wb[1] -= (p[2] + kb[11]) * fpx;
+            wb[2] += (p[1] + kb[10]) * fpx;
+            wb[3] -= fpx;
+        }
+    }
     wave_sync();
     /* Plucker columns for the muscle-path lanes: held in registers when they
      * fit beside the muscle state (planar models), read from LDS otherwise
@@ -1316,10 +1361,15 @@ template <class T, typename Real> struct LaunchArgs {
     uint8_t *done_out;
     const int32_t *env_ids, *ref_index;
     uint64_t seed;
+    /* apply_perturbations: zero-order-hold force table x[pert_n] (shared),
+     * y[pert_n][N]; force on OpenSim body pert_ob; pert_n == 0: off */
+    const double *pert_x;
+    const Real *pert_y;
+    int pert_n, pert_ob;
 };
 
 /* One 256-thread workgroup = 256/G envs of segment `a`, block `blk`. */
-template <class T, typename Real>
+template <class T, typename Real, bool PERT>
 DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     using LY = Lay<T, Real>;
     constexpr int G = T::G, ND = LY::ND, NA = T::NA, NM = T::NM;
@@ -1395,6 +1445,9 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
 
     int remaining = 0;
     Real dt = 0;
+    const PertArgs<Real> PA{a.pert_x, a.pert_y, a.pert_n, a.pert_ob, env, N};
+    double *pslot = reinterpret_cast<double *>(smem_raw + SMB + sizeof(Real) * EPB * LY::SIZE) + PERT_SLOT * slot;
+    if (PERT && lane == 0) { pslot[0] = t; pslot[1] = 0; pslot[2] = 0; pslot[3] = -1; pslot[4] = 0; }
     if (mode == 0) {
         /* ---- action pre-processing (Env.step) */
         Real raw[MPL];
@@ -1447,6 +1500,17 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
                 if (hh < H) sm += hist[j][hh];
             curr[j] = sm / Real(H);
+            if constexpr (PERT) {
+                /* the deque is final here: store it now instead of holding it
+                 * in registers through the substep loop (the push kernels
+                 * carry the table cursor; this keeps their register count at
+                 * or below the default kernels') */
+                if (m < NA) {
+#pragma unroll
+                    for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
+                        if (hh < H) st.hist[((size_t)hh * NA + m) * N + env] = hist[j][hh];
+                }
+            }
             const Real phys = (M.env_flags & BIOIM_ENV_RAW_ACTION) ? av[j] : curr[j];
             pnan_here = pnan_here || (m < NA && isnan(phys));
             control[j] = phys;
@@ -1468,6 +1532,8 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         if (hstep > 0) {
             dt = Real(hstep / (double)M.nsub);
             remaining = M.nsub;
+            /* substep k starts at t + k * hstep / nsub (the oracle's substep times) */
+            if (PERT && lane == 0) { pslot[0] = t; pslot[1] = hstep / (double)M.nsub; }
         }
         t = tf;
     }
@@ -1500,8 +1566,10 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             typedef const __attribute__((address_space(4))) DModel<Real> CModel;
             CModel *Mi = (CModel *)Mg;
             asm volatile("" : "+s"(Mi));
-            dynamics<T, Real>(*(const DModel<Real> *)Mi, SM, qd, ud, act, lce, control, lane, lds, sub ? dt : Real(0),
-                              eq && NM > 0, D);
+            /* realize / reset realize: the call time is t itself */
+            if (PERT && !sub && lane == 0) { pslot[0] = t; pslot[1] = 0; }
+            dynamics<T, Real, PERT>(*(const DModel<Real> *)Mi, SM, qd, ud, act, lce, control, lane, lds, sub ? dt : Real(0),
+                              eq && NM > 0, PA, pslot, M.nsub - remaining, D);
         }
         if (sub) {
             if (lane < ND) { ud += dt * D.qdd; qd += dt * ud; }
@@ -1751,16 +1819,18 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         if (NM > 0 && m < NM) { st.act[(size_t)m * N + env] = act[j]; st.lce[(size_t)m * N + env] = lce[j]; }
         if (m < NA) {
             st.last[(size_t)m * N + env] = last[j];
+            if (!PERT) {
 #pragma unroll
-            for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
-                if (hh < H) st.hist[((size_t)hh * NA + m) * N + env] = hist[j][hh];
+                for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
+                    if (hh < H) st.hist[((size_t)hh * NA + m) * N + env] = hist[j][hh];
+            }
         }
     }
 }
 
-template <class T, typename Real>
+template <class T, typename Real, bool PERT>
 __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))) void env_kernel(LaunchArgs<T, Real> a) {
-    env_block<T, Real>(a, blockIdx.x);
+    env_block<T, Real, PERT>(a, blockIdx.x);
 }
 
 
@@ -2035,14 +2105,17 @@ struct bioim_handle {
     void *state_buf;    /* one allocation for every SoA array */
     size_t state_bytes;
     void *dstate;       /* DState<Real> (host copy of pointers) */
+    void *pert_x, *pert_y; /* apply_perturbations table: double [pert_n], Real [pert_n][n] */
+    int pert_n, pert_ob;
     Ops ops;
     bioim_modelpack_t pack;
 };
 
 namespace {
 
-template <class T, typename Real> constexpr size_t lds_bytes() {
-    return smodel_bytes<T, Real>() + (size_t)(BIOIM_WG / T::G) * Lay<T, Real>::SIZE * sizeof(Real);
+template <class T, typename Real, bool PERT = false> constexpr size_t lds_bytes() {
+    return smodel_bytes<T, Real>() + (size_t)(BIOIM_WG / T::G) * Lay<T, Real>::SIZE * sizeof(Real) +
+           (PERT ? (size_t)(BIOIM_WG / T::G) * PERT_SLOT * sizeof(double) : 0);
 }
 
 template <class T, typename Real>
@@ -2064,6 +2137,9 @@ LaunchArgs<T, Real> make_args(bioim_handle_t *h, int mode, const void *actions, 
     a.done_out = done;
     a.env_ids = env_ids; a.ref_index = ref_index;
     a.seed = h->seed;
+    a.pert_x = reinterpret_cast<const double *>(h->pert_x);
+    a.pert_y = reinterpret_cast<const Real *>(h->pert_y);
+    a.pert_n = h->pert_n; a.pert_ob = h->pert_ob;
     return a;
 }
 
@@ -2072,14 +2148,23 @@ void launch_impl(bioim_handle_t *h, int mode, const void *actions, void *obs, vo
                  const int32_t *env_ids, const int32_t *ref_index, int n_list) {
     LaunchArgs<T, Real> a = make_args<T, Real>(h, mode, actions, obs, reward, done, info, env_ids, ref_index, n_list);
     if (a.blocks <= 0) return;
-    constexpr size_t lds = lds_bytes<T, Real>();
-    hipLaunchKernelGGL((env_kernel<T, Real>), dim3(a.blocks), dim3(BIOIM_WG), lds, h->stream, a);
+    /* the perturbation kernels are separate instantiations, so the default
+     * kernels' code is untouched by the (rarely used) push */
+    if (a.pert_n > 0) {
+        constexpr size_t lds = lds_bytes<T, Real, true>();
+        hipLaunchKernelGGL((env_kernel<T, Real, true>), dim3(a.blocks), dim3(BIOIM_WG), lds, h->stream, a);
+    } else {
+        constexpr size_t lds = lds_bytes<T, Real, false>();
+        hipLaunchKernelGGL((env_kernel<T, Real, false>), dim3(a.blocks), dim3(BIOIM_WG), lds, h->stream, a);
+    }
 }
 
 template <class T, typename Real> int upload_smodel(bioim_handle_t *h) {
-    static_assert(lds_bytes<T, Real>() <= 163840, "LDS image + env regions exceed 160 KiB");
-    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real>()));
+    static_assert(lds_bytes<T, Real, true>() <= 163840, "LDS image + env regions exceed 160 KiB");
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, false>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, false>()));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, true>()));
     constexpr size_t B = smodel_bytes<T, Real>();
     std::vector<unsigned char> img(B, 0);
     build_smodel<T, Real>(h->pack, *reinterpret_cast<SModel<T, Real> *>(img.data()));
@@ -2218,6 +2303,7 @@ int bioim_create(const bioim_modelpack_t *pack, int n_envs, int device, int prec
     h->ndof = pack->ndof; h->nmuscle = pack->nmuscle; h->nact = pack->nact; h->horizon = pack->horizon;
     h->obs_dim = pack->obs_dim; h->info_dim = pack->info_dim; h->nsub = pack->nsub; h->auto_reset = 0;
     h->env_offset = 0;
+    h->pert_n = 0; h->pert_ob = -1;
     h->act_stride = pack->nact; h->obs_stride = pack->obs_dim; h->info_stride = pack->info_dim;
     h->ops = ops;
     memcpy(&h->pack, pack, sizeof(bioim_modelpack_t));
@@ -2244,6 +2330,8 @@ int bioim_destroy(bioim_handle_t *h) {
     if (h->state_buf) hipFree(h->state_buf);
     if (h->model) hipFree(h->model);
     if (h->smodel) hipFree(h->smodel);
+    if (h->pert_x) hipFree(h->pert_x);
+    if (h->pert_y) hipFree(h->pert_y);
     if (h->dstate) {
         if (h->precision == 64) delete reinterpret_cast<DState<double> *>(h->dstate);
         else delete reinterpret_cast<DState<float> *>(h->dstate);
@@ -2327,6 +2415,36 @@ int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs
         off += (size_t)h->n;
     }
     HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int bioim_set_perturbation(bioim_handle_t *h, int os_body, int npts, const double *x, const double *y) {
+    if (!h || npts < 0 || (npts > 0 && (!x || !y || os_body < 0 || os_body >= h->pack.nosbody)))
+        return fail(BIOIM_E_ARG, "bioim_set_perturbation: bad arguments");
+    for (int k = 0; k + 1 < npts; ++k)
+        if (!(x[k] < x[k + 1])) return fail(BIOIM_E_ARG, "bioim_set_perturbation: breakpoints must increase");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipStreamSynchronize(h->side));
+    if (h->pert_x) { HIPCHK(hipFree(h->pert_x)); h->pert_x = nullptr; }
+    if (h->pert_y) { HIPCHK(hipFree(h->pert_y)); h->pert_y = nullptr; }
+    h->pert_n = 0;
+    h->pert_ob = -1;
+    if (npts == 0) return 0;
+    const size_t n = h->n, R = h->precision == 64 ? 8 : 4;
+    std::vector<unsigned char> yt(R * n * npts);   /* [npts][n], env index fastest */
+    for (size_t e = 0; e < n; ++e)
+        for (int k = 0; k < npts; ++k) {
+            const double v = y[e * npts + k];
+            if (R == 8) reinterpret_cast<double *>(yt.data())[k * n + e] = v;
+            else reinterpret_cast<float *>(yt.data())[k * n + e] = (float)v;
+        }
+    HIPCHK(hipMalloc(&h->pert_x, sizeof(double) * npts));
+    HIPCHK(hipMalloc(&h->pert_y, yt.size()));
+    HIPCHK(hipMemcpy(h->pert_x, x, sizeof(double) * npts, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->pert_y, yt.data(), yt.size(), hipMemcpyHostToDevice));
+    h->pert_n = npts;
+    h->pert_ob = os_body;
     return 0;
 }
 

@@ -97,6 +97,15 @@ int bioim_set_io_strides(bioim_handle_t *h, int act_stride, int obs_stride, int 
  * heterogeneous sub-envs. */
 int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs, void *reward, uint8_t *done,
                      void *info);
+/* apply_perturbations (muscle_walking_imitation_env2D.py:83-100 and the same
+ * block in every task env): a PrescribedForce on the torso whose ground-frame
+ * x force is a PiecewiseConstantFunction of simulation time.  Here: a
+ * zero-order-hold table per env — force y[e][k] on [x[k], x[k+1]) (y[e][0]
+ * before x[0]) along ground x, applied at the origin of OpenSim body
+ * `os_body` (ModelPack osbody index) at every substep and realize.  x: host
+ * double[npts], strictly increasing, shared by all envs; y: host double
+ * [N][npts].  npts = 0 removes the force.  Synchronous (copies to device). */
+int bioim_set_perturbation(bioim_handle_t *h, int os_body, int npts, const double *x, const double *y);
 /* Global index of this handle's env 0 (multi-GPU sharding): device-drawn
  * reset indices depend on the global env index, so a sharded run is
  * bit-identical to an unsharded one. */

@@ -38,6 +38,7 @@ class Oracle:
             ('orc_get_state', None, [C.c_void_p, C.c_void_p, _dp]),
             ('orc_set_state', None, [C.c_void_p, C.c_void_p, _dp]),
             ('orc_env_init', None, [C.c_void_p]),
+            ('orc_env_set_perturbation', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, _dp, _dp]),
             ('orc_forward_kinematics', None, [C.c_void_p, _dp, _dp, _dp, _dp]),
             ('orc_mass_matrix_bias', None, [C.c_void_p, _dp, _dp, _dp, _dp]),
             ('orc_forward_dynamics', C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
@@ -82,6 +83,14 @@ class Oracle:
         self.lib.orc_env_step(self.pk, self.env_ptr(envs, i), _ptr(a), _ptr(obs), _ptr(rew), C.byref(done),
                               _ptr(info))
         return obs, float(rew[0]), bool(done.value), info
+
+    def set_perturbation(self, envs, i, os_body, x, y):
+        """Zero-order-hold torso force table of env i (see orc_env_t)"""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        rc = self.lib.orc_env_set_perturbation(self.pk, self.env_ptr(envs, i), int(os_body), len(x), _ptr(x), _ptr(y))
+        if rc:
+            raise ValueError('orc_env_set_perturbation: bad table')
 
     def state_dim(self):
         return self.lib.orc_state_dim(self.pk)

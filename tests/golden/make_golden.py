@@ -53,6 +53,7 @@ _load_by_path('bioim_amd.curves', os.path.join(PKG, 'curves.py'))
 _load_by_path('bioim_amd.modelpack', os.path.join(PKG, 'modelpack.py'))
 registry = _load_by_path('bioim_amd.registry', os.path.join(PKG, 'registry.py'))
 storage = _load_by_path('bioim_amd.storage', os.path.join(PKG, 'storage.py'))
+perturb = _load_by_path('bioim_amd.perturb', os.path.join(PKG, 'perturb.py'))
 sys.path.insert(0, os.path.join(REPO, 'oracle'))
 import oracle as oracle_mod  # noqa: E402
 import ctypes as C  # noqa: E402
@@ -60,6 +61,42 @@ import ctypes as C  # noqa: E402
 # ------------------------------------------------------------------ stubs
 opensim = types.ModuleType('opensim')
 sys.modules['opensim'] = opensim
+
+
+class _Constant:
+    def __init__(self, v):
+        self.value = float(v)
+
+
+class _PiecewiseConstantFunction:
+    """Records the points the reference adds (muscle_walking_imitation_env2D.py:89-95)."""
+
+    def __init__(self):
+        self.x, self.y = [], []
+
+    def addPoint(self, x, y):
+        self.x.append(float(x))
+        self.y.append(float(y))
+
+
+class _PrescribedForce:
+    def __init__(self):
+        self.body = None
+        self.points = self.forces = None
+
+    def setBodyName(self, name):
+        self.body = name
+
+    def setPointFunctions(self, *f):
+        self.points = f
+
+    def setForceFunctions(self, *f):
+        self.forces = f
+
+
+opensim.Constant = _Constant
+opensim.PiecewiseConstantFunction = _PiecewiseConstantFunction
+opensim.PrescribedForce = _PrescribedForce
 gym = types.ModuleType('gym')
 
 
@@ -172,6 +209,12 @@ class _Model:
 
     def getMuscles(self):
         return _Set([_Muscle(self.fm, i) for i in range(self.fm.pack.nmuscle)])
+
+    def addForce(self, f):
+        self.fm.add_prescribed_force(f)
+
+    def initSystem(self):
+        return None
 
 
 class FakeOsimModel:
@@ -319,6 +362,17 @@ class FakeOsimModel:
     def get_action_space_size(self):
         return len(self.action_min)
 
+    def add_prescribed_force(self, f):
+        """The torso push: body origin, ground-x PiecewiseConstantFunction, others Constant(0)"""
+        assert all(isinstance(p, _Constant) and p.value == 0.0 for p in f.points)
+        assert all(isinstance(p, _Constant) and p.value == 0.0 for p in f.forces[1:])
+        fx = f.forces[0]
+        body = f.body.split('/')[-1]
+        ob = self.names['bodies'].index(body)
+        xt, yt = perturb.zoh_table(fx.x, fx.y)
+        self.orc.set_perturbation(self.envbuf, 0, ob, xt, yt)
+        CURRENT['perturbation'] = (body, np.array(fx.x), np.array(fx.y))
+
 
 oenv.OsimModel = FakeOsimModel
 
@@ -389,7 +443,54 @@ def run_episode(env, pk, seed, T, action_fn, nan_at=()):
                 done=np.array(done), info=np.array(info), obs_keys=np.array(keys))
 
 
+def main_perturbations():
+    """apply_perturbations episodes (tests/golden/perturbations.npz): the
+    reference's own schedule draw (np.random seeded) and steps through pushes."""
+    out = {}
+    cases = [('TorqueWalkingImitation2D-v0', 'torque.planar.torque_walking_imitation_env2D',
+              'TorqueWalkingImitationEnv2D', 132, 70),
+             ('MuscleWalkingImitation2D-v0', 'muscle.planar.muscle_walking_imitation_env2D',
+              'MuscleWalkingImitationEnv2D', 132, 70),
+             ('MuscleRunningImitation3D-v0', 'muscle.spatial.muscle_running_imitation_env3D',
+              'MuscleRunningImitationEnv3D', None, 30),
+             ('MusclePalsyImitation3D-v0', 'muscle.spatial.muscle_palsy_imitation_env3D',
+              'MusclePalsyImitationEnv3D', None, 20)]
+    rng = np.random.Generator(np.random.PCG64(11))
+    for j, (env_id, modfile, cls, index, T) in enumerate(cases):
+        config = dict(DEFAULT_CFG, apply_perturbations=True)
+        np.random.seed(100 + j)
+        env, pk = make_env(env_id, 'bioimitation.imitation_envs.envs.' + modfile, cls, config)
+        body, px, py = CURRENT['perturbation']
+        hi = pk.reset_hi
+        seed = 7000 + j if index is None else seed_for_index(min(index, hi), hi)
+        if pk.nmuscle:
+            acts = rng.uniform(0.0, 0.3, size=(T, pk.nact))
+
+            def act(t, e, acts=acts):
+                return acts[t].copy()
+        else:
+            noise = rng.normal(0.0, 0.02, size=(T, pk.nact))
+            pdc = [CURRENT['names']['coords'][pk.pd_coord[i]] for i in range(pk.nact)]
+
+            def act(t, e, noise=noise, pdc=pdc):
+                row = e.q_d.iloc[min(e.osim_model.istep + 1, len(e.q_d) - 1)]
+                return np.array([row[c] for c in pdc]) + noise[t]
+        ep = run_episode(env, pk, seed, T, act)
+        ep.update(config=repr(config), env_id=env_id, np_seed=100 + j, body=body, px=px, py=py)
+        out[f'ep{j}'] = ep
+        t_end = 0.01 * (ep['index'] + len(ep['reward']))
+        print(env_id, 'perturbation episode index', ep['index'], 'steps', len(ep['reward']), 'done', ep['done'][-1],
+              f't_end {t_end:.2f}', 'pushes', py[py != 0][:4])
+    flat = {f'{k}_{f}': np.asarray(v) for k, ep in out.items() for f, v in ep.items()}
+    flat['n_episodes'] = np.array(len(out))
+    path = os.path.join(HERE, 'perturbations.npz')
+    np.savez_compressed(path, **flat)
+    print('wrote', path)
+
+
 def main():
+    if '--perturbations' in sys.argv:
+        return main_perturbations()
     out = {}
     # ---------------- MuscleWalkingImitation2D-v0
     mod = 'bioimitation.imitation_envs.envs.muscle.planar.muscle_walking_imitation_env2D'

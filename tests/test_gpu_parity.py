@@ -283,3 +283,87 @@ def test_mixed_batch_matches_separate_envs(segments):
     assert mixed.action_mask.sum().item() == sum(e.num_envs * e.action_dim for e in alone)
     for e in alone + [mixed]:
         e.close()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+@pytest.mark.parametrize('env_id', ['TorqueWalkingImitation2D-v0', 'MuscleWalkingImitation2D-v0',
+                                    'MuscleRunningImitation3D-v0', 'MuscleLockedKneeImitation3D-v0'])
+def test_perturbation_parity_fp64(env_id):
+    """apply_perturbations (muscle_walking_imitation_env2D.py:83-100): the
+    torso push evaluated per substep on the device vs the oracle, fp64,
+    free-running.  The tables are dense random pushes (every 0.03 s a new
+    value in {-50, 0, 50} N per env) so every env sees several switches within
+    the 30 steps, including switches inside a step's substeps; the reference's
+    own schedule shape is pinned host-side (tests/test_golden.py)."""
+    import torch
+    from bioimitation.obslayout import load_names
+    from bioimitation.perturb import os_body_index, zoh_table
+    rng = np.random.default_rng(9)
+    n, T = 32, 30
+    rows = rng.integers(0, 120, size=n)
+    pk, env, orc, bufs = _setup(env_id, n, 64)
+    x = np.arange(0.0, 3.0, 0.03) + 0.0013
+    y = rng.choice([-50.0, 0.0, 50.0], size=(n, len(x)))
+    env.set_perturbation(x, y)
+    ob = os_body_index(load_names(env_id))
+    xt, _ = zoh_table(x, y)
+    for i in range(n):
+        orc.set_perturbation(bufs, i, ob, xt, y[i])
+    env.reset(ref_index=rows)
+    for i in range(n):
+        orc.reset(bufs, i, int(rows[i]))
+    alive = np.ones(n, bool)
+    worst = 0.0
+    for t in range(T):
+        st = np.array([orc.get_state(bufs, i)[1] for i in range(n)]).astype(int)
+        acts = _actions(env_id, rng, n, env.action_dim, pk, st + 1)
+        if 'Muscle' in env_id:
+            acts *= 0.4
+        obs, rew, done, info = env.step(torch.as_tensor(acts, device=env.device))
+        torch.cuda.synchronize()
+        obs, rew, done, info = (v.cpu().numpy() for v in (obs, rew, done, info))
+        for i in range(n):
+            if not alive[i]:
+                continue
+            o, r, d, inf = orc.step(bufs, i, acts[i])
+            e = max(_rel(obs[i], o).max(), abs(rew[i] - r), _rel(info[i], inf).max())
+            assert e < 1e-6, (t, i, e)
+            assert bool(done[i]) == d, (t, i)
+            worst = max(worst, e)
+            alive[i] = alive[i] and not d
+    print(f'{env_id} perturbed fp64 {T} steps: max rel err {worst:.2e}, alive {alive.sum()}/{n}')
+    # the push is live: removing it changes the trajectory
+    env.set_perturbation(None, None)
+    env.reset(ref_index=rows)
+    a = torch.as_tensor(_actions(env_id, rng, n, env.action_dim, pk, rows + 1), device=env.device)
+    o_free = env.step(a)[0].clone()
+    env.set_perturbation(x, y)
+    env.reset(ref_index=rows)
+    o_push = env.step(a)[0]
+    assert not torch.equal(o_free, o_push)
+    env.close()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+def test_perturbation_config_sharded():
+    """config apply_perturbations=True draws per-env schedules keyed by the
+    global env index: two sharded handles reproduce one unsharded handle."""
+    import torch
+    from bioimitation.vector_env import VectorEnv
+    env_id, total, cfg = 'TorqueWalkingImitation2D-v0', 64, {'apply_perturbations': True, 'perturbation_seed': 4}
+    full = VectorEnv(env_id, total, config=cfg, precision=64, seed=3, auto_reset=True)
+    parts = [VectorEnv(env_id, 40, config=cfg, precision=64, seed=3, auto_reset=True),
+             VectorEnv(env_id, 24, config=cfg, precision=64, seed=3, auto_reset=True, env_offset=40)]
+    np.testing.assert_array_equal(full.perturbation[1], np.concatenate([p.perturbation[1] for p in parts]))
+    rows = np.full(total, 160)    # t = 1.6: the 1.5-threshold pushes start at 1.515
+    full.reset(ref_index=rows)
+    parts[0].reset(ref_index=rows[:40])
+    parts[1].reset(ref_index=rows[40:])
+    for t in range(25):
+        a = torch.as_tensor(np.tile([full.pack.ref_q[min(161 + t, full.pack.nrows - 1)][full.pack.pd_coord[i]]
+                                     for i in range(full.action_dim)], (total, 1)), device=full.device)
+        o = full.step(a)[0]
+        o2 = torch.cat([parts[0].step(a[:40].contiguous())[0], parts[1].step(a[40:].contiguous())[0]])
+        assert torch.equal(o, o2), t
+    for e in [full] + parts:
+        e.close()
