@@ -104,6 +104,13 @@ class ImitationEnv:
         self.spec.action_space = self.action_space
         self.spec.observation_space = self.observation_space
         self._names = None
+        # the OsimModel facade callers reach through env.osim_model (save_simulation, istep, ...)
+        from .obslayout import load_names
+        from .simulation_io import OsimModelFacade
+        self.osim_model = OsimModelFacade(self._env, load_names(self.env_id), lo, hi)
+        self._record = bool(cfg.get('record_trajectory', True))
+        ntrans = sum(1 for c in (pk.coord_tx, pk.coord_ty, pk.coord_tz) if c >= 0)
+        self._qdd = slice(1 + (pk.ncoord - ntrans) + pk.ncoord, 1 + (pk.ncoord - ntrans) + 2 * pk.ncoord)
 
     # -- reference API -------------------------------------------------------
     def _out(self, obs, as_dict):
@@ -115,9 +122,15 @@ class ImitationEnv:
             self._names = load_names(self.env_id)
         return obs_to_dict(o, self._env.pack, self._names)
 
+    def _record_row(self, obs):
+        if self._record:
+            self.osim_model.recorder.record(self._env.get_state()[0], obs[0, self._qdd].double().cpu().numpy())
+
     def reset(self, obs_as_dict=False):
         index = 0 if self.test else random.randint(0, self._env.pack.reset_hi)
         obs = self._env.reset(env_ids=[0], ref_index=[index])
+        self.osim_model.recorder.clear()     # reset_manager re-initializes the analyses
+        self._record_row(obs)
         return self._out(obs, obs_as_dict)
 
     def step(self, action, obs_as_dict=False):
@@ -125,6 +138,7 @@ class ImitationEnv:
         a = torch.as_tensor(np.asarray(action, dtype=np.float64).reshape(1, -1), dtype=self._env.dtype,
                             device=self._env.device)
         obs, rew, done, info = self._env.step(a)
+        self._record_row(obs)
         info = info[0].double().cpu().numpy()
         return [self._out(obs, obs_as_dict), float(rew[0]), bool(done[0]),
                 {'all_rewards': [float(v) for v in info]}]

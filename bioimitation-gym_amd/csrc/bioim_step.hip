@@ -1345,6 +1345,188 @@ DEV int draw_index(uint64_t seed, int env, int count, int hi) {
     return (int)(r % (uint64_t)(hi + 1));
 }
 
+
+/* ------------------------------------------------- inverse dynamics
+ * Batched primitives of the reference's Boost.Python InverseDynamics helper
+ * (bioimitation/imitation_envs/inverse_dynamics/inverse_dynamics.cpp:45-205),
+ * muscles disabled (:47-52), no controller (actuator controls 0).  One
+ * state per G lanes, the env kernel's LDS image and kinematics:
+ *   GRAVITY   g(q)            M q'' + c = g + tau           (:127-141)
+ *   CORIOLIS  c(q, u)                                       (:143-158)
+ *   MULT_M    M(q) v                                        (:160-175)
+ *   MULT_MINV M(q)^-1 v                                     (:177-192)
+ *   RESIDUAL  M v + c - f_applied(q, u), v = q''            (:63-94)
+ *   TOTAL     c - f_applied(q, u)  (M q'' + f = tau)        (:96-125)
+ * f_applied = gravity + Hunt-Crossley contact + coordinate limit forces
+ * (generalized).  Vectors are [n][ndof] in dof order. */
+template <class T, typename Real> struct IdArgs {
+    const DModel<Real> *Mg;
+    const SModel<T, Real> *Sg;
+    int n, op;
+    const Real *q, *u, *v;
+    Real *out;
+};
+
+template <class T, typename Real>
+__global__ __launch_bounds__(BIOIM_WG) void id_kernel(IdArgs<T, Real> a) {
+    using LY = Lay<T, Real>;
+    constexpr int G = T::G, ND = LY::ND, NB = T::NB, NP = LY::NP, EPB = BIOIM_WG / G;
+    constexpr size_t SMB = smodel_bytes<T, Real>();
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.Sg);
+        uint4 *dst = reinterpret_cast<uint4 *>(smem_raw);
+        for (int i = threadIdx.x; i < (int)(SMB / 16); i += BIOIM_WG) dst[i] = src[i];
+    }
+    __syncthreads();
+    const SModel<T, Real> &SM = *reinterpret_cast<const SModel<T, Real> *>(smem_raw);
+    const DModel<Real> &M = *a.Mg;
+    const int lane = threadIdx.x % G, slot = threadIdx.x / G;
+    const int idx = blockIdx.x * EPB + slot;
+    if (idx >= a.n) return;
+    Real *lds = reinterpret_cast<Real *>(smem_raw + SMB) + slot * LY::SIZE;
+    const int op = a.op;
+    const bool use_u = op == BIOIM_ID_CORIOLIS || op == BIOIM_ID_RESIDUAL || op == BIOIM_ID_TOTAL;
+    const bool applied = op == BIOIM_ID_RESIDUAL || op == BIOIM_ID_TOTAL;
+    const bool need_m = op == BIOIM_ID_MULT_M || op == BIOIM_ID_MULT_MINV || op == BIOIM_ID_RESIDUAL;
+    Real qd = 0, ud = 0, vd = 0;
+    if (lane < ND) {
+        qd = a.q[(size_t)idx * ND + lane];
+        ud = use_u ? a.u[(size_t)idx * ND + lane] : Real(0);
+        vd = (need_m || op == BIOIM_ID_MULT_MINV) ? a.v[(size_t)idx * ND + lane] : Real(0);
+    }
+    publish_coords<T, Real>(M, SM, lds, lane, qd, ud);
+    if (lane < ND) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) lds[LY::SL + 6 * lane + i] = 0;
+    }
+    wave_sync();
+    Real x0 = 0;
+    if constexpr (T::TX >= 0) {
+        if constexpr (T::coord_dof[T::TX] >= 0) x0 = M.float_origin ? lds[LY::QF + T::TX] : Real(0);
+    }
+    if (lane < NB) kin_local<T, Real>(SM, lds, lane);
+    if (lane == NB) kin_ground<T, Real>(lds, x0);
+    wave_sync();
+    if (lane < NB) kin_chain<T, Real>(SM, lds, lane, x0);
+    wave_sync();
+    if (lane < ND) kin_column<T, Real>(SM, lds, lane);
+    if (lane < NB) {
+        body_inertia<T, Real>(SM, M, lds, lane);
+        if (op == BIOIM_ID_CORIOLIS) {   /* velocity terms only: take the gravity wrench back out */
+            const Real *kb = lds + LY::KB + 18 * lane;
+            Real cG[3], mg[3], t[3];
+            mv3(kb, SM.body[lane].com, cG);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { cG[i] += kb[9 + i]; mg[i] = SM.body[lane].mass * M.gravity[i]; }
+            cross3(cG, mg, t);
+            Real *wb = lds + LY::WB + 6 * lane;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { wb[i] += t[i]; wb[3 + i] += mg[i]; }
+        }
+    }
+    wave_sync();
+    {   /* subtree sums of inertia and wrench (all reads, then all writes) */
+        Real ic[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, wb[6] = {0, 0, 0, 0, 0, 0};
+        if (lane < NB) {
+            sfor<0, NB>([&](auto dI) {
+                constexpr int d = decltype(dI)::value;
+                if ((T::anc[d] >> lane) & 1u) {
+#pragma unroll
+                    for (int i = 0; i < 10; ++i) ic[i] += lds[LY::IC + 10 * d + i];
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) wb[i] += lds[LY::WB + 6 * d + i];
+                }
+            });
+        }
+        wave_sync();
+        if (lane < NB) {
+#pragma unroll
+            for (int i = 0; i < 10; ++i) lds[LY::IC + 10 * lane + i] = ic[i];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) lds[LY::WB + 6 * lane + i] = wb[i];
+        }
+    }
+    if (applied) {
+        if (lane < T::NS) contact_lane<T, Real>(SM, lds, lane, Real(0));
+        if (lane < T::NL) {
+            const int cc = SM.lim_coord[lane];
+            const Real qv = lds[LY::QF + cc], qdv = lds[LY::UF + cc];
+            const Real qup = SM.lim_qup[lane], qlo = SM.lim_qlow[lane], tr = SM.lim_trans[lane];
+            const Real up = smooth_step(Real(0), Real(1), qup, qup + tr, qv);
+            const Real lo = smooth_step(Real(1), Real(0), qlo - tr, qlo, qv);
+            lds[LY::LIM + 4 * lane] = -SM.lim_kup[lane] * up * (qv - qup) + SM.lim_klow[lane] * lo * (qlo - qv) -
+                                      SM.lim_damp[lane] * (up + lo) * qdv;
+        }
+    }
+    wave_sync();
+    if (need_m) {
+        for (int e = lane; e < NP; e += G) {
+            const int l = SM.e_l[e], k = SM.e_k[e], c = SM.e_c[e];
+            const Real *Sl = lds + LY::S + 6 * l, *Sk = lds + LY::S + 6 * k;
+            Real val = 0;
+            if (c >= 0) {
+                const Real *ic = lds + LY::IC + 10 * c;
+                Real Lm[3], Pm[3], t[3];
+                symv(ic + 4, Sl, Lm);
+                cross3(ic + 1, Sl + 3, t);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) Lm[i] += t[i];
+                cross3(Sl, ic + 1, t);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) Pm[i] = ic[0] * Sl[3 + i] + t[i];
+                val = dot3(Sk, Lm) + dot3(Sk + 3, Pm);
+            }
+            lds[LY::MP + e] = val;
+        }
+    }
+    if (lane < ND) lds[LY::RHS + lane] = vd;
+    wave_sync();
+    Real r = 0;
+    if (op == BIOIM_ID_MULT_MINV) {
+        Real A[NP], xs[ND];
+#pragma unroll
+        for (int e = 0; e < NP; ++e) A[e] = lds[LY::MP + e];
+#pragma unroll
+        for (int d = 0; d < ND; ++d) xs[d] = lds[LY::RHS + d];
+        cholesky_solve<ND, Real>(A, xs);
+#pragma unroll
+        for (int d = 0; d < ND; ++d) r = lane == d ? xs[d] : r;
+    } else if (lane < ND) {
+        const Real *Sd = lds + LY::S + 6 * lane, *wb = lds + LY::WB + 6 * SM.dof_cb[lane];
+        const Real bias = dot3(Sd, wb) + dot3(Sd + 3, wb + 3);   /* c - g (gravity removed for CORIOLIS) */
+        Real fa = 0;
+        if (applied) {
+            sfor<0, T::NS>([&](auto sI) {
+                constexpr int sp = decltype(sI)::value;
+                constexpr unsigned msk = T::dofmask[T::sphere_cb[sp]];
+                const Real *cj = lds + LY::CJ + LY::CJN * sp;
+                Real jd[3];
+                contact_jac(Sd, cj, jd);
+                const Real term = dot3(jd, cj + 3);
+                fa += (lds[LY::CW + 8 * sp + 6] > 0 && ((msk >> lane) & 1u)) ? term : Real(0);
+            });
+#pragma unroll
+            for (int li = 0; li < T::NL; ++li)
+                if (SM.lim_dof[li] == lane) fa += lds[LY::LIM + 4 * li];
+        }
+        Real mv = 0;
+        if (need_m) {
+#pragma unroll
+            for (int k = 0; k < ND; ++k) {
+                const int hi = lane > k ? lane : k, lo = lane > k ? k : lane;
+                mv += lds[LY::MP + hi * (hi + 1) / 2 + lo] * lds[LY::RHS + k];
+            }
+        }
+        if (op == BIOIM_ID_GRAVITY) r = -bias;
+        else if (op == BIOIM_ID_CORIOLIS) r = bias;
+        else if (op == BIOIM_ID_MULT_M) r = mv;
+        else if (op == BIOIM_ID_RESIDUAL) r = mv + bias - fa;
+        else r = bias - fa;
+    }
+    if (lane < ND) a.out[(size_t)idx * ND + lane] = r;
+}
+
 /* ---------------------------------------------------------------- kernel
  * Launch arguments of one env segment (one handle).  mode 0: env step
  * (optionally with in-kernel auto-reset); mode 1: reset the listed envs.
@@ -2088,6 +2270,7 @@ struct Ops {
     int (*upload)(bioim_handle_t *);
     void (*launch)(bioim_handle_t *, int mode, const void *actions, void *obs, void *reward, uint8_t *done, void *info,
                    const int32_t *env_ids, const int32_t *ref_index, int n_list);
+    void (*id_launch)(bioim_handle_t *, int op, int n, const void *q, const void *u, const void *v, void *out);
 };
 
 }  // namespace
@@ -2159,12 +2342,27 @@ void launch_impl(bioim_handle_t *h, int mode, const void *actions, void *obs, vo
     }
 }
 
+template <class T, typename Real>
+void id_launch_impl(bioim_handle_t *h, int op, int n, const void *q, const void *u, const void *v, void *out) {
+    constexpr int EPB = BIOIM_WG / T::G;
+    IdArgs<T, Real> a;
+    a.Mg = reinterpret_cast<const DModel<Real> *>(h->model);
+    a.Sg = reinterpret_cast<const SModel<T, Real> *>(h->smodel);
+    a.n = n; a.op = op;
+    a.q = reinterpret_cast<const Real *>(q); a.u = reinterpret_cast<const Real *>(u);
+    a.v = reinterpret_cast<const Real *>(v); a.out = reinterpret_cast<Real *>(out);
+    constexpr size_t lds = lds_bytes<T, Real, false>();
+    hipLaunchKernelGGL((id_kernel<T, Real>), dim3((n + EPB - 1) / EPB), dim3(BIOIM_WG), lds, h->stream, a);
+}
+
 template <class T, typename Real> int upload_smodel(bioim_handle_t *h) {
     static_assert(lds_bytes<T, Real, true>() <= 163840, "LDS image + env regions exceed 160 KiB");
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, false>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, false>()));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, true>()));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&id_kernel<T, Real>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, false>()));
     constexpr size_t B = smodel_bytes<T, Real>();
     std::vector<unsigned char> img(B, 0);
     build_smodel<T, Real>(h->pack, *reinterpret_cast<SModel<T, Real> *>(img.data()));
@@ -2180,10 +2378,12 @@ template <class T> bool pick(const bioim_modelpack_t &p, int precision, Ops &ops
     ops.lanes = T::G;
     if (precision == 64) {
         ops.launch = &launch_impl<T, double>;
+        ops.id_launch = &id_launch_impl<T, double>;
         ops.upload = &upload_smodel<T, double>;
         ops.lds_bytes = lds_bytes<T, double>();
     } else {
         ops.launch = &launch_impl<T, float>;
+        ops.id_launch = &id_launch_impl<T, float>;
         ops.upload = &upload_smodel<T, float>;
         ops.lds_bytes = lds_bytes<T, float>();
     }
@@ -2445,6 +2645,19 @@ int bioim_set_perturbation(bioim_handle_t *h, int os_body, int npts, const doubl
     HIPCHK(hipMemcpy(h->pert_y, yt.data(), yt.size(), hipMemcpyHostToDevice));
     h->pert_n = npts;
     h->pert_ob = os_body;
+    return 0;
+}
+
+int bioim_id_eval(bioim_handle_t *h, int op, int n, const void *q, const void *u, const void *v, void *out) {
+    if (!h || n < 0 || op < BIOIM_ID_GRAVITY || op > BIOIM_ID_TOTAL || (n > 0 && (!q || !out)))
+        return fail(BIOIM_E_ARG, "bioim_id_eval: bad arguments");
+    const bool use_u = op == BIOIM_ID_CORIOLIS || op == BIOIM_ID_RESIDUAL || op == BIOIM_ID_TOTAL;
+    const bool use_v = op == BIOIM_ID_MULT_M || op == BIOIM_ID_MULT_MINV || op == BIOIM_ID_RESIDUAL;
+    if (n > 0 && ((use_u && !u) || (use_v && !v))) return fail(BIOIM_E_ARG, "bioim_id_eval: missing u or v");
+    if (n == 0) return 0;
+    HIPCHK(hipSetDevice(h->device));
+    h->ops.id_launch(h, op, n, q, u, v, out);
+    HIPCHK(hipGetLastError());
     return 0;
 }
 

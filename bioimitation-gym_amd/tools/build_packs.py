@@ -54,7 +54,10 @@ def main():
         out = os.path.join(DATA, 'packs', env_id + '.npz')
         names = dict(coords=list(model.coord_order), bodies=list(model.body_order),
                      muscles=[mu.name for mu in model.muscles] if pk.nmuscle else [],
-                     cforces=[h.name for h in model.hc_forces], limits=[l.name for l in model.limits])
+                     cforces=[h.name for h in model.hc_forces], limits=[l.name for l in model.limits],
+                     coord_joints=[model.coords[c].joint for c in model.coord_order],
+                     coord_rotational=[c not in _translational(model) for c in model.coord_order],
+                     coord_locked=[bool(model.coords[c].locked) for c in model.coord_order])
         np.savez_compressed(out, pack=np.frombuffer(modelpack.pack_bytes(pk), dtype=np.uint8),
                             names=np.array(json.dumps(names)))
         built.append((env_id, pk))
@@ -70,6 +73,21 @@ def main():
 def _carr(name, vals, ctype='int'):
     vals = list(vals) or [0]
     return f'    static constexpr {ctype} {name}[{len(vals)}] = {{{", ".join(str(int(v)) for v in vals)}}};\n'
+
+
+def _translational(model):
+    """Coordinates that drive a CustomJoint translation axis and no rotation
+    axis (OpenSim 4 derives the motion type from the spatial transform; 3.x
+    files also state it)."""
+    out = {c for c, co in model.coords.items() if co.motion == 'translational'}
+    rot = set()
+    for j in model.joints:
+        for ax in (j.axes or []):
+            if ax.coord and ax.name.startswith('rotation'):
+                rot.add(ax.coord)
+            elif ax.coord and ax.name.startswith('translation'):
+                out.add(ax.coord)
+    return out - rot
 
 
 def unique_curves(pk):

@@ -106,6 +106,27 @@ int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs
  * double[npts], strictly increasing, shared by all envs; y: host double
  * [N][npts].  npts = 0 removes the force.  Synchronous (copies to device). */
 int bioim_set_perturbation(bioim_handle_t *h, int os_body, int npts, const double *x, const double *y);
+/* Inverse-dynamics primitives of the reference's InverseDynamics helper
+ * (bioimitation/imitation_envs/inverse_dynamics/inverse_dynamics.cpp:45-205;
+ * Boost.Python, built against OpenSim) on the handle's model, batched over n
+ * states: muscles disabled, actuator controls 0, the model's gravity,
+ * Hunt-Crossley contact and coordinate limit forces.  q, u, v, out: device
+ * [n][ndof] in the handle's precision, dof order (locked coordinates are not
+ * dofs).  `u` is read by CORIOLIS/RESIDUAL/TOTAL, `v` by MULT_M/MULT_MINV/
+ * RESIDUAL.  Conventions (inverse_dynamics.cpp comments): M q'' + c = g + tau;
+ * RESIDUAL = M v + c - f_applied (calculateResidualForces, :63-94); TOTAL =
+ * c - f_applied, i.e. M q'' + f = tau (calculateTotalForces, :96-125);
+ * GRAVITY = g (:127-141); CORIOLIS = c (:143-158); MULT_M = M v (:160-175);
+ * MULT_MINV = M^-1 v (:177-192).  Asynchronous on the handle's stream. */
+enum {
+    BIOIM_ID_GRAVITY = 0,
+    BIOIM_ID_CORIOLIS = 1,
+    BIOIM_ID_MULT_M = 2,
+    BIOIM_ID_MULT_MINV = 3,
+    BIOIM_ID_RESIDUAL = 4,
+    BIOIM_ID_TOTAL = 5,
+};
+int bioim_id_eval(bioim_handle_t *h, int op, int n, const void *q, const void *u, const void *v, void *out);
 /* Global index of this handle's env 0 (multi-GPU sharding): device-drawn
  * reset indices depend on the global env index, so a sharded run is
  * bit-identical to an unsharded one. */

@@ -38,6 +38,7 @@ class Oracle:
             ('orc_get_state', None, [C.c_void_p, C.c_void_p, _dp]),
             ('orc_set_state', None, [C.c_void_p, C.c_void_p, _dp]),
             ('orc_env_init', None, [C.c_void_p]),
+            ('orc_id_eval', C.c_int, [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp]),
             ('orc_env_set_perturbation', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, _dp, _dp]),
             ('orc_forward_kinematics', None, [C.c_void_p, _dp, _dp, _dp, _dp]),
             ('orc_mass_matrix_bias', None, [C.c_void_p, _dp, _dp, _dp, _dp]),
@@ -140,6 +141,16 @@ class Oracle:
         args = [np.ascontiguousarray(x, dtype=np.float64) for x in (q, u, act, lce, controls)]
         rc = self.lib.orc_forward_dynamics(self.pk, *[_ptr(x) for x in args], _ptr(qdd), _ptr(mo))
         return qdd, mo, rc
+
+    def id_eval(self, op, q, u=None, v=None):
+        """inverse-dynamics primitive op (include/bioim.h BIOIM_ID_*), per-dof vectors"""
+        nd = self.pack.ndof
+        z = np.zeros(nd)
+        q, u, v = (np.ascontiguousarray(z if x is None else x, dtype=np.float64) for x in (q, u, v))
+        out = np.zeros(nd)
+        if self.lib.orc_id_eval(self.pk, int(op), _ptr(q), _ptr(u), _ptr(v), _ptr(out)):
+            raise ValueError('orc_id_eval failed (M not SPD?)')
+        return out
 
     def muscle_path(self, q, u, m):
         L, Ld = C.c_double(), C.c_double()

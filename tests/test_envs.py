@@ -60,3 +60,88 @@ def test_single_env_matches_oracle(env_id):
     d = env.step(env.action_space.sample(rng), obs_as_dict=True)[0]      # the reference's nested dict
     assert set(d) >= {'phase', 'coordinate_pos', 'coordinate_vel', 'body_pos'} and len(d['body_pos']) == 10
     env.close()
+
+
+def test_trajectory_recorder_writes_opensim_storage(tmp_path):
+    """save_simulation's files (opensim_wrapper.py:334-338) from recorded
+    rows: OpenSim 4 state paths, Kinematics in degrees for rotational
+    coordinates, locked coordinates at their defaults.  Host logic only."""
+    import math
+    from bioimitation.obslayout import load_names
+    from bioimitation.registry import load_pack
+    from bioimitation.simulation_io import TrajectoryRecorder
+    from bioimitation.storage import read_sto
+    env_id = 'MuscleLockedKneeImitation3D-v0'
+    pk, names = load_pack(env_id), load_names(env_id)
+    rec = TrajectoryRecorder(pk, names)
+    rng = np.random.default_rng(0)
+    dim = 5 + 2 * pk.ndof + 2 * pk.nmuscle + pk.horizon * pk.nact + pk.nact
+    rows = []
+    for k in range(4):
+        s = rng.normal(size=dim)
+        s[0] = 0.3 + 0.01 * k
+        rows.append(s)
+        rec.record(s, rng.normal(size=pk.ncoord))
+    paths = rec.write(str(tmp_path))
+    h, labels, data = read_sto(paths['states'])
+    assert data.shape == (4, 1 + 2 * pk.ncoord + 2 * pk.nmuscle)
+    c = names['coords'].index('hip_flexion_r')
+    j = names['coord_joints'][c]
+    col = labels.index(f'/jointset/{j}/hip_flexion_r/value')
+    d = pk.coord[c].dof
+    np.testing.assert_allclose(data[:, col], [r[5 + d] for r in rows], atol=1e-9)
+    locked = names['coords'].index('knee_angle_l')
+    assert names['coord_locked'][locked]
+    np.testing.assert_allclose(data[:, labels.index(f'/jointset/{names["coord_joints"][locked]}/knee_angle_l/speed')], 0)
+    m0 = names['muscles'][0]
+    np.testing.assert_allclose(data[:, labels.index(f'/forceset/{m0}/activation')], [r[5 + 2 * pk.ndof] for r in rows])
+    hq, lq, dq = read_sto(paths['q'])
+    assert hq['inDegrees'] == 'yes' and lq[1:] == names['coords']
+    np.testing.assert_allclose(dq[:, 1 + c], data[:, col] * 180 / math.pi, atol=1e-6)
+    tx = names['coords'].index('pelvis_tx')
+    np.testing.assert_allclose(dq[:, 1 + tx], [r[5 + pk.coord[tx].dof] for r in rows], atol=1e-9)   # metres
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+def test_single_env_save_simulation_and_perturbation(tmp_path):
+    """env.osim_model.save_simulation after an episode (tests/sample_rllib_testing.py:71)
+    holds the reset row plus one row per step, matching the oracle; and
+    apply_perturbations draws its schedule from NumPy's global RNG like the
+    reference (np.random.seed reproduces it)."""
+    import oracle
+    from bioimitation import envs
+    from bioimitation.obslayout import load_names
+    from bioimitation.perturb import os_body_index, reference_points, zoh_table
+    from bioimitation.registry import load_pack
+    from bioimitation.storage import read_sto
+    env_id = 'TorqueWalkingImitation2D-v0'
+    cfg = {'mode': 'train', 'apply_perturbations': True}
+    np.random.seed(5)
+    env = envs.make(env_id, cfg)
+    np.random.seed(5)
+    x, y = reference_points(env_id)
+    np.testing.assert_array_equal(env._env.perturbation[1][0], y)
+    pk = load_pack(env_id, cfg)
+    orc = oracle.Oracle(pk)
+    bufs = orc.new_envs(1)
+    orc.set_perturbation(bufs, 0, os_body_index(load_names(env_id)), *zoh_table(x, y))
+    random.seed(1)
+    env.reset()
+    random.seed(1)
+    orc.reset(bufs, 0, random.randint(0, pk.reset_hi))
+    states = [orc.get_state(bufs, 0)]
+    for t in range(6):
+        a = np.array([pk.ref_q[min(env.osim_model.istep + 1, pk.nrows - 1)][pk.pd_coord[i]] for i in range(pk.nact)])
+        o, r, d, _ = env.step(a)
+        ro, rr, rd, _ = orc.step(bufs, 0, a)
+        np.testing.assert_allclose(o, ro, rtol=1e-7, atol=1e-7)
+        states.append(orc.get_state(bufs, 0))
+    paths = env.osim_model.save_simulation(str(tmp_path))
+    h, labels, data = read_sto(paths['states'])
+    assert data.shape[0] == 7
+    np.testing.assert_allclose(data[:, 0], [s[0] for s in states], atol=1e-9)
+    c = load_names(env_id)['coords'].index('knee_angle_r')
+    col = labels.index('/jointset/knee_r/knee_angle_r/value')
+    np.testing.assert_allclose(data[:, col], [s[5 + pk.coord[c].dof] for s in states], atol=1e-8)
+    env.close()
