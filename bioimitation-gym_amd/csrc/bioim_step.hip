@@ -2016,10 +2016,18 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
 }
 
 
-/* =================================================================== host */
-namespace {
+/* =================================================================== host
+ * Build modes (the library links 8 objects compiled in parallel):
+ *   BIOIM_TOPO_ONLY=k  the kernels and host launchers of topology k only
+ *                      (bioim_pick_k);
+ *   BIOIM_ABI_ONLY     the C-ABI, no kernels;
+ *   neither            everything in one translation unit (diagnostic builds). */
+#if defined(BIOIM_TOPO_ONLY) && defined(BIOIM_ABI_ONLY)
+#error "BIOIM_TOPO_ONLY and BIOIM_ABI_ONLY are exclusive"
+#endif
+extern thread_local std::string g_err;   /* bioim_last_error(); defined with the C-ABI */
 
-thread_local std::string g_err;
+namespace {
 
 int fail(int code, const std::string &msg) {
     g_err = msg;
@@ -2264,6 +2272,8 @@ template <class T> bool topology_matches(const bioim_modelpack_t &p) {
     return true;
 }
 
+}  // namespace
+
 struct Ops {
     int lanes;
     size_t lds_bytes;   /* per workgroup: model image + BIOIM_WG / lanes env regions */
@@ -2272,8 +2282,6 @@ struct Ops {
                    const int32_t *env_ids, const int32_t *ref_index, int n_list);
     void (*id_launch)(bioim_handle_t *, int op, int n, const void *q, const void *u, const void *v, void *out);
 };
-
-}  // namespace
 
 struct bioim_handle {
     int n, device, precision, ndof, nmuscle, nact, horizon, obs_dim, info_dim, nsub, auto_reset, env_offset;
@@ -2472,6 +2480,26 @@ template <typename Real> int xfer_state(bioim_handle_t *h, double *host, const d
 
 }  // namespace
 
+/* topology k's kernel table (one object per topology, or all in this TU) */
+#define BIOIM_PICK_DECL(S, NAME) bool bioim_pick_##S(const bioim_modelpack_t &p, int precision, Ops &ops);
+BIOIM_FOR_EACH_TOPOLOGY(BIOIM_PICK_DECL)
+#undef BIOIM_PICK_DECL
+#ifndef BIOIM_ABI_ONLY
+#define BIOIM_PICK_DEF(S, NAME)                                                      \
+    bool bioim_pick_##S(const bioim_modelpack_t &p, int precision, Ops &ops) { return pick<S>(p, precision, ops); }
+#ifdef BIOIM_TOPO_ONLY
+#define BIOIM_PICK_ONE(S, NAME) BIOIM_PICK_DEF(S, NAME)
+BIOIM_TOPOLOGY_AT(BIOIM_TOPO_ONLY, BIOIM_PICK_ONE)
+#undef BIOIM_PICK_ONE
+#else
+BIOIM_FOR_EACH_TOPOLOGY(BIOIM_PICK_DEF)
+#endif
+#undef BIOIM_PICK_DEF
+#endif
+
+#ifndef BIOIM_TOPO_ONLY
+thread_local std::string g_err;
+
 /* ================================================================ C-ABI */
 extern "C" {
 
@@ -2494,7 +2522,7 @@ int bioim_create(const bioim_modelpack_t *pack, int n_envs, int device, int prec
     Ops ops{};
     bool found = false;
 #define BIOIM_TRY(S, NAME) \
-    if (!found) found = pick<S>(*pack, precision, ops);
+    if (!found) found = bioim_pick_##S(*pack, precision, ops);
     BIOIM_FOR_EACH_TOPOLOGY(BIOIM_TRY)
 #undef BIOIM_TRY
     if (!found) return fail(BIOIM_E_NOKERNEL, std::string("bioim_create: no compiled kernel for the topology of ") + pack->env_id);
@@ -2732,3 +2760,4 @@ int bioim_sync(bioim_handle_t *h) {
 }
 
 }  // extern "C"
+#endif  // BIOIM_TOPO_ONLY

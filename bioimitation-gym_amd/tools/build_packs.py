@@ -200,6 +200,13 @@ def write_topologies(packs):
     out.append('#define BIOIM_FOR_EACH_TOPOLOGY(X) \\')
     out.append(' \\\n'.join(f'    X({s}, "{e}")' for e, s in names))
     out.append('')
+    # one topology by index: the per-topology objects of the library build (__graft_entry__.py)
+    out.append(f'#define BIOIM_NTOPOLOGIES {len(names)}')
+    out.append('#define BIOIM_TOPOLOGY_AT(k, X) BIOIM_TOPOLOGY_AT_I(k, X)')
+    out.append('#define BIOIM_TOPOLOGY_AT_I(k, X) BIOIM_TOPOLOGY_AT_##k(X)')
+    for k, (e, s_) in enumerate(names):
+        out.append(f'#define BIOIM_TOPOLOGY_AT_{k}(X) X({s_}, "{e}")')
+    out.append('')
     path = os.path.join(PKG_ROOT, 'csrc', 'topologies.h')
     with open(path, 'w') as fh:
         fh.write('\n'.join(out))
