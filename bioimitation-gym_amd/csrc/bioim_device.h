@@ -11,6 +11,8 @@
 
 #define BIOIM_OBS_MAX 256
 
+#define BIOIM_MAX_SPAN 8 /* muscle span: non-root dofs per muscle (max) */
+
 #define BIOIM_UTAB 32 /* intervals of the per-segment u(x) initial-guess table */
 
 template <typename Real>
@@ -35,6 +37,11 @@ struct SMuscle {
     Real tau_act, tau_deact, amin, beta, width, lmin, slow, mass, default_act, pad;
     int32_t pt_off, npt;
     int32_t cv[4]; /* curve indices: fal, fv, fpe, fse */
+    /* non-root dofs the path can move (union of its points' dofmasks minus
+     * the floating base: a muscle's force is internal, so its generalized
+     * force on the root dofs is zero) */
+    int32_t nspan, pad2;
+    int32_t span[BIOIM_MAX_SPAN];
 };
 
 template <typename Real>

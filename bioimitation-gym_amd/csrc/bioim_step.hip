@@ -916,14 +916,30 @@ DEV Real muscle_equilibrium(const SModel<T, Real> &SM, const SMuscle<Real> &mu, 
  * from registers (loaded once per dynamics call).  Fixed trip count over
  * the topology's maximum point count; only the point indices that can be
  * conditional / moving (compile-time masks) carry that code. */
-template <class T, typename Real, class SA>
-DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const Real *lds, const SA &S, Real &L,
-                     Real *dLdq) {
+/* Path length L and the moment arms dL/dq over the muscle's span (dLs[k]
+ * for dof mu.span[k], k < mu.nspan): per active point the
+ * change of the unit direction g acts at the point, dL/dq_d += S_d . (P x g, g)
+ * for the dofs moving the point, plus g . dP/dq for a moving point's own
+ * coordinate.  The floating-base dofs are skipped: their sum over a path is
+ * zero (sum g = 0, sum P x g = 0).  The span's Plucker columns are read from
+ * LDS once per muscle into registers. */
+template <class T, typename Real>
+DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const Real *lds, Real &L,
+                     Real (&dLs)[T::MAXSPAN]) {
     using LY = Lay<T, Real>;
+    constexpr int NSP = T::MAXSPAN;
     const Real *ldsq = lds + LY::QF;
     L = 0;
+    int sd[NSP];
+    Real Ss[NSP][6];
 #pragma unroll
-    for (int d = 0; d < T::ND; ++d) dLdq[d] = 0;
+    for (int k = 0; k < NSP; ++k) {
+        dLs[k] = 0;
+        sd[k] = k < mu.nspan ? mu.span[k] : -1;
+        const int dk = k < mu.nspan ? mu.span[k] : 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) Ss[k][i] = lds[LY::S + 6 * dk + i];
+    }
     Real Pp[3] = {0, 0, 0}, ep[3] = {0, 0, 0}, dPp[3] = {0, 0, 0};
     uint32_t maskp = 0;
     int mdofp = -1;
@@ -931,12 +947,14 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
     auto flush = [&](const Real *g) {
         Real mo[3];
         cross3(Pp, g, mo);
+        const Real gd = dot3(g, dPp);
 #pragma unroll
-        for (int d = 0; d < T::ND; ++d) {
-            Real on = (maskp >> d) & 1u ? Real(1) : Real(0);
-            const Real sm = S(d, 0) * mo[0] + S(d, 1) * mo[1] + S(d, 2) * mo[2];
-            const Real sg = S(d, 3) * g[0] + S(d, 4) * g[1] + S(d, 5) * g[2];
-            dLdq[d] += on * (sm + sg) + (mdofp == d ? dot3(g, dPp) : Real(0));
+        for (int k = 0; k < NSP; ++k) {
+            const int d = sd[k];
+            const Real on = d >= 0 && ((maskp >> d) & 1u) ? Real(1) : Real(0);
+            const Real sm = Ss[k][0] * mo[0] + Ss[k][1] * mo[1] + Ss[k][2] * mo[2];
+            const Real sg = Ss[k][3] * g[0] + Ss[k][4] * g[1] + Ss[k][5] * g[2];
+            dLs[k] += on * (sm + sg) + (mdofp == d && d >= 0 ? gd : Real(0));
         }
     };
     const int npt = mu.npt;
@@ -1085,21 +1103,6 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
         }
     }
     wave_sync();
-    /* Plucker columns for the muscle-path lanes: held in registers when they
-     * fit beside the muscle state (planar models), read from LDS otherwise
-     * (the spatial models' 14 columns would spill) */
-    constexpr bool SREG = ND <= 9;
-    Real Sr[SREG ? ND : 1][6];
-    if constexpr (SREG) {
-#pragma unroll
-        for (int d = 0; d < ND; ++d)
-#pragma unroll
-            for (int i = 0; i < 6; ++i) Sr[d][i] = lds[LY::S + 6 * d + i];
-    }
-    const auto Sget = [&](int d, int i) -> Real {
-        if constexpr (SREG) return Sr[d][i];
-        else return lds[LY::S + 6 * d + i];
-    };
     STAMP(2);
 
     /* ---- phase 2: lane-parallel force elements */
@@ -1126,6 +1129,11 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     }
     STAMP(3);
     if constexpr (T::NM > 0) {
+        /* this lane's muscles' -F_t dL/dq over their spans, accumulated in
+         * registers (compile-time dof indices) and stored as one torque
+         * slot.  (An LDS read-modify-write of the slot at the span's runtime
+         * dof indices, combined with the early deque store, produced wrong
+         * fp32 3D results on the GPU — DESIGN.md 5.1.) */
         Real tau[ND];
 #pragma unroll
         for (int d = 0; d < ND; ++d) tau[d] = 0;
@@ -1134,8 +1142,8 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
             const int m = lane + j * G;
             if (m < T::NM) {
                 const SMuscle<Real> &mu = SM.mus[m];
-                Real L, dLdq[ND];
-                muscle_path<T, Real>(SM, mu, lds, Sget, L, dLdq);
+                Real L, dLs[T::MAXSPAN];
+                muscle_path<T, Real>(SM, mu, lds, L, dLs);
                 STAMP(4);
                 Real a_ = act[j], l_ = lce[j];
                 if (equilibrate) { /* reset: default activation, static fiber equilibrium */
@@ -1145,8 +1153,13 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
                 D.act[j] = a_;
                 D.lce[j] = l_;
                 muscle_eval<T, Real>(SM, mu, a_, l_, control[j], L, D.ms[j].vN, D.ms[j]);
+                const Real nFt = -D.ms[j].Ft;
 #pragma unroll
-                for (int d = 0; d < ND; ++d) tau[d] += -D.ms[j].Ft * dLdq[d];
+                for (int k = 0; k < T::MAXSPAN; ++k) {
+                    const int dk = k < mu.nspan ? mu.span[k] : -1;
+#pragma unroll
+                    for (int d = 0; d < ND; ++d) tau[d] += dk == d ? nFt * dLs[k] : Real(0);
+                }
             }
         });
         if (lane < LY::NTL) {
@@ -1682,16 +1695,12 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
                 if (hh < H) sm += hist[j][hh];
             curr[j] = sm / Real(H);
-            if constexpr (PERT) {
-                /* the deque is final here: store it now instead of holding it
-                 * in registers through the substep loop (the push kernels
-                 * carry the table cursor; this keeps their register count at
-                 * or below the default kernels') */
-                if (m < NA) {
+            /* the deque is final here: store it now instead of holding it in
+             * registers through the substep loop (34 AGPRs in 3D fp64) */
+            if (m < NA) {
 #pragma unroll
-                    for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
-                        if (hh < H) st.hist[((size_t)hh * NA + m) * N + env] = hist[j][hh];
-                }
+                for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
+                    if (hh < H) st.hist[((size_t)hh * NA + m) * N + env] = hist[j][hh];
             }
             const Real phys = (M.env_flags & BIOIM_ENV_RAW_ACTION) ? av[j] : curr[j];
             pnan_here = pnan_here || (m < NA && isnan(phys));
@@ -2001,11 +2010,6 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         if (NM > 0 && m < NM) { st.act[(size_t)m * N + env] = act[j]; st.lce[(size_t)m * N + env] = lce[j]; }
         if (m < NA) {
             st.last[(size_t)m * N + env] = last[j];
-            if (!PERT) {
-#pragma unroll
-                for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
-                    if (hh < H) st.hist[((size_t)hh * NA + m) * N + env] = hist[j][hh];
-            }
         }
     }
 }
@@ -2133,6 +2137,14 @@ template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, 
         d.width = (Real)s.width; d.lmin = (Real)s.lmin; d.slow = (Real)s.slow_twitch; d.mass = (Real)s.mass;
         d.default_act = (Real)s.default_act; d.pt_off = s.pt_off; d.npt = s.npt;
         for (int k = 0; k < 4; ++k) d.cv[k] = cidx[4 * i + k];
+        uint32_t root = ~0u, u = 0;
+        for (int c = 0; c < T::NB; ++c) root &= T::dofmask[c];
+        for (int j = 0; j < s.npt; ++j) u |= T::dofmask[p.pathpt[s.pt_off + j].cbody];
+        u &= ~root;
+        d.nspan = 0;
+        for (int dd = 0; dd < T::ND; ++dd)
+            if ((u >> dd) & 1u) d.span[d.nspan++] = dd;
+        for (int k = d.nspan; k < BIOIM_MAX_SPAN; ++k) d.span[k] = d.nspan ? d.span[0] : 0;
     }
     std::vector<uint32_t> dofmask(T::NB, 0);
     for (int c = 0; c < T::NB; ++c) dofmask[c] = T::dofmask[c];

@@ -149,7 +149,18 @@ def emit_topology(struct, pk, lanes):
             t = pk.pathpt[m.pt_off + j].type
             cond |= (1 << j) if t == 1 else 0
             move |= (1 << j) if t == 2 else 0
+    root = (1 << nd) - 1
+    for c in range(nb):
+        root &= dofmask[c]
+    maxspan = 1
+    for i in range(pk.nmuscle):
+        m = pk.muscle[i]
+        u = 0
+        for j in range(m.npt):
+            u |= dofmask[pk.pathpt[m.pt_off + j].cbody]
+        maxspan = max(maxspan, bin(u & ~root).count('1'))
     s += f'    static constexpr int MAXPT = {maxpt}; /* path points per muscle (max) */\n'
+    s += f'    static constexpr int MAXSPAN = {maxspan}; /* non-root dofs a muscle path moves (max) */\n'
     s += f'    static constexpr unsigned PT_COND = {cond}u, PT_MOVING = {move}u; /* point indices that can be conditional / moving */\n'
     s += f'    static constexpr int TX = {pk.coord_tx}, TY = {pk.coord_ty}, TZ = {pk.coord_tz};\n'
     s += f'    static constexpr int TORSO = {pk.torso_body}, CALCN_R = {pk.calcn_r_body}, CALCN_L = {pk.calcn_l_body};\n'
