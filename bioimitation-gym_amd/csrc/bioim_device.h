@@ -17,8 +17,11 @@
 
 template <typename Real>
 struct DCurve {
-    Real x[BIOIM_MAX_CURVESEG][6];
-    Real y[BIOIM_MAX_CURVESEG][6];
+    /* per quintic segment: x(u), y(u) in the power basis (Horner), from the
+     * pack's Bernstein control points; x/y at u = 0 and u = 1 */
+    Real cx[BIOIM_MAX_CURVESEG][6];
+    Real cy[BIOIM_MAX_CURVESEG][6];
+    Real xa[BIOIM_MAX_CURVESEG], xb[BIOIM_MAX_CURVESEG], ya[BIOIM_MAX_CURVESEG], yb[BIOIM_MAX_CURVESEG];
     Real ut[BIOIM_MAX_CURVESEG][BIOIM_UTAB + 1]; /* u at uniform x nodes of each segment */
     Real inv_h[BIOIM_MAX_CURVESEG];               /* BIOIM_UTAB / (x_end - x_start)       */
     Real x0, y0, dydx0, x1, y1, dydx1;

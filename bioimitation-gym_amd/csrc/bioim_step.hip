@@ -214,15 +214,14 @@ DEV void sincos_rt(double x, double &s, double &c) {
 DEV void sincos_rt(float x, float &s, float &c) { sincosf(x, &s, &c); }
 
 /* ----------------------------------------------------- smooth curves */
-template <typename Real> DEV Real bez5(const Real *p, Real u) {
-    Real v = Real(1) - u, u2 = u * u, v2 = v * v;
-    return p[0] * v2 * v2 * v + Real(5) * p[1] * u * v2 * v2 + Real(10) * p[2] * u2 * v2 * v +
-           Real(10) * p[3] * u2 * u * v2 + Real(5) * p[4] * u2 * u2 * v + p[5] * u2 * u2 * u;
+/* a quintic segment in the power basis c[0] + c[1] u + ... + c[5] u^5
+ * (converted from the Bezier control points at create time, convert_curve):
+ * Horner, 5 FMAs; the derivative 4 */
+template <typename Real> DEV Real bez5(const Real *c, Real u) {
+    return fma(fma(fma(fma(fma(c[5], u, c[4]), u, c[3]), u, c[2]), u, c[1]), u, c[0]);
 }
-template <typename Real> DEV Real dbez5(const Real *p, Real u) {
-    Real v = Real(1) - u, u2 = u * u, v2 = v * v;
-    return Real(5) * ((p[1] - p[0]) * v2 * v2 + Real(4) * (p[2] - p[1]) * u * v2 * v +
-                      Real(6) * (p[3] - p[2]) * u2 * v2 + Real(4) * (p[4] - p[3]) * u2 * u * v + (p[5] - p[4]) * u2 * u2);
+template <typename Real> DEV Real dbez5(const Real *c, Real u) {
+    return fma(fma(fma(fma(Real(5) * c[5], u, Real(4) * c[4]), u, Real(3) * c[3]), u, Real(2) * c[2]), u, c[1]);
 }
 
 /* y(x), dy/dx of a SmoothSegmentedFunction.  Branch-free with a fixed trip
@@ -235,11 +234,11 @@ DEV void curve_eval(const DCurve<Real> &C, Real x, Real &y, Real &dydx) {
     Real xc = x < C.x0 ? C.x0 : (x > C.x1 ? C.x1 : x);
     int k = 0;
 #pragma unroll
-    for (int s = 0; s < BIOIM_MAX_CURVESEG - 1; ++s) k += (s < C.nseg - 1 && xc > C.x[s][5]) ? 1 : 0;
+    for (int s = 0; s < BIOIM_MAX_CURVESEG - 1; ++s) k += (s < C.nseg - 1 && xc > C.xb[s]) ? 1 : 0;
     Real px[6], py[6];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) { px[i] = C.x[k][i]; py[i] = C.y[k][i]; }
-    Real tt = (xc - px[0]) * C.inv_h[k];
+    for (int i = 0; i < 6; ++i) { px[i] = C.cx[k][i]; py[i] = C.cy[k][i]; }
+    Real tt = (xc - C.xa[k]) * C.inv_h[k];
     int i0 = (int)tt;
     i0 = i0 < 0 ? 0 : (i0 > BIOIM_UTAB - 1 ? BIOIM_UTAB - 1 : i0);
     Real fr = tt - Real(i0);
@@ -263,14 +262,15 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
     Real g1 = afal * C.y1 + beta * C.x1 - rhs;
     int k = 0;
 #pragma unroll
-    for (int s = 1; s < BIOIM_MAX_CURVESEG; ++s) k += (s < C.nseg && afal * C.y[s][0] + beta * C.x[s][0] - rhs <= 0) ? 1 : 0;
+    for (int s = 1; s < BIOIM_MAX_CURVESEG; ++s) k += (s < C.nseg && afal * C.ya[s] + beta * C.xa[s] - rhs <= 0) ? 1 : 0;
     Real px[6], py[6];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) { px[i] = C.x[k][i]; py[i] = C.y[k][i]; }
-    Real ga = afal * py[0] + beta * px[0] - rhs, gb = afal * py[5] + beta * px[5] - rhs;
+    for (int i = 0; i < 6; ++i) { px[i] = C.cx[k][i]; py[i] = C.cy[k][i]; }
+    const Real xa = C.xa[k], xb = C.xb[k];
+    Real ga = afal * C.ya[k] + beta * xa - rhs, gb = afal * C.yb[k] + beta * xb - rhs;
     Real u;
-    if (v0 > px[0] && v0 < px[5]) {
-        Real tt = (v0 - px[0]) * C.inv_h[k];
+    if (v0 > xa && v0 < xb) {
+        Real tt = (v0 - xa) * C.inv_h[k];
         int i0 = (int)tt;
         i0 = i0 < 0 ? 0 : (i0 > BIOIM_UTAB - 1 ? BIOIM_UTAB - 1 : i0);
         Real fr = tt - Real(i0);
@@ -279,11 +279,16 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
         u = ga / (ga - gb);
     }
     u = u > Real(0) && u < Real(1) ? u : Real(0.5);
+    /* g(u) = a fal y(u) + beta x(u) - rhs is one quintic in u */
+    Real pg[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) pg[i] = afal * py[i] + beta * px[i];
+    pg[0] -= rhs;
     Real lo = 0, hi = 1, dprev = 1;
     for (int it = 0; it < Eps<Real>::it_max; ++it) {
-        Real g = afal * bez5(py, u) + beta * bez5(px, u) - rhs;
+        Real g = bez5(pg, u);
         if (g > 0) hi = u; else lo = u;
-        Real dg = afal * dbez5(py, u) + beta * dbez5(px, u);
+        Real dg = dbez5(pg, u);
         Real un = u - g / dg;
         /* inclusive bracket: a converged step (un == u == lo or hi after
          * rounding) must not trigger the bisection fallback */
@@ -2060,9 +2065,29 @@ double host_invert(const double *px, double x) {
     return 0.5 * (lo + hi);
 }
 
+/* Bernstein control points of a quintic -> power-basis coefficients:
+ * c_j = C(5, j) sum_{k <= j} C(j, k) (-1)^(j-k) p_k */
+void bernstein_to_power(const double *p, double *c) {
+    static const double B5[6] = {1, 5, 10, 10, 5, 1};
+    for (int j = 0; j < 6; ++j) {
+        double s = 0, bjk = 1;   /* C(j, k) */
+        for (int k = 0; k <= j; ++k) {
+            s += bjk * (((j - k) & 1) ? -p[k] : p[k]);
+            bjk = bjk * (j - k) / (k + 1);
+        }
+        c[j] = B5[j] * s;
+    }
+}
+
 template <typename Real> void convert_curve(const bioim_curve_t &s, DCurve<Real> &d) {
-    for (int i = 0; i < BIOIM_MAX_CURVESEG; ++i)
-        for (int j = 0; j < 6; ++j) { d.x[i][j] = (Real)s.x[i][j]; d.y[i][j] = (Real)s.y[i][j]; }
+    for (int i = 0; i < BIOIM_MAX_CURVESEG; ++i) {
+        double cx[6], cy[6];
+        bernstein_to_power(s.x[i], cx);
+        bernstein_to_power(s.y[i], cy);
+        for (int j = 0; j < 6; ++j) { d.cx[i][j] = (Real)cx[j]; d.cy[i][j] = (Real)cy[j]; }
+        d.xa[i] = (Real)s.x[i][0]; d.xb[i] = (Real)s.x[i][5];
+        d.ya[i] = (Real)s.y[i][0]; d.yb[i] = (Real)s.y[i][5];
+    }
     for (int k = 0; k < BIOIM_MAX_CURVESEG; ++k) {
         if (k >= s.nseg) { d.inv_h[k] = 0; for (int i = 0; i <= BIOIM_UTAB; ++i) d.ut[k][i] = 0; continue; }
         double a = s.x[k][0], b = s.x[k][5];
