@@ -320,6 +320,38 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
     }
 }
 
+/* composite bodies carrying contact spheres (the feet), in first-appearance
+ * order of T::sphere_cb */
+template <class T> struct Feet {
+    static constexpr int count() {
+        int n = 0;
+        for (int s = 0; s < T::NS; ++s) {
+            bool seen = false;
+            for (int r = 0; r < s; ++r) seen = seen || T::sphere_cb[r] == T::sphere_cb[s];
+            n += seen ? 0 : 1;
+        }
+        return n;
+    }
+    static constexpr int N = count();
+    static constexpr int cb(int i) {   /* composite body of foot i */
+        int n = 0;
+        for (int s = 0; s < T::NS; ++s) {
+            bool seen = false;
+            for (int r = 0; r < s; ++r) seen = seen || T::sphere_cb[r] == T::sphere_cb[s];
+            if (!seen) {
+                if (n == i) return T::sphere_cb[s];
+                ++n;
+            }
+        }
+        return -1;
+    }
+    static constexpr int of(int sp) {  /* foot index of sphere sp */
+        for (int i = 0; i < N; ++i)
+            if (cb(i) == T::sphere_cb[sp]) return i;
+        return 0;
+    }
+};
+
 /* ---------------------------------------------------------- LDS layout
  * Per workgroup: the shared model image (SModel, bioim_device.h), then one
  * region per env.  Phase 1 (lane-parallel kinematics) publishes frames,
@@ -356,7 +388,9 @@ template <class T, typename Real> struct Lay {
     static constexpr int CJ = TAU + NTL * ND;    /* phases 2-3: [NS][CJN] contact slots             */
     static constexpr int OBS = U;                /* report: observation staging                     */
     static constexpr int REP = OBS + OBSMAX;     /* report: [NOS+1][6] body pos/vel (NOS: COM)      */
-    static constexpr int U1 = 24 * (NB + 1) + 6 * ND, U2 = NTL * ND + NS * CJN;
+    static constexpr int NFB = Feet<T>::N;       /* feet: phase-3 implicit contact vectors [NFB][ND][6] at TAU */
+    static constexpr int U2A = NTL * ND + NS * CJN, U2B = 6 * NFB * ND;
+    static constexpr int U1 = 24 * (NB + 1) + 6 * ND, U2 = U2A > U2B ? U2A : U2B;
     static constexpr int U3 = OBSMAX + 6 * (T::NOS + 1);
     static constexpr int USZ = U1 > U2 ? (U1 > U3 ? U1 : U3) : (U2 > U3 ? U2 : U3);
     static constexpr int SIZE = ((U + USZ + 1) / 2) * 2;
@@ -371,6 +405,10 @@ DEV void wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+/* the same fence inside a lane-divergent region: orders this wave's LDS
+ * accesses (the active lanes' reads before their writes); lanes of one wave
+ * execute in lockstep, so no lane can be behind */
+DEV void wave_sync_lanes() { wave_sync(); }
 
 /* Diagnostic build only (-DBIOIM_STAMPS, tools/stamps.py): per-phase shader
  * cycles of the first env of workgroup 0, accumulated over one launch. */
@@ -1215,7 +1253,59 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     wave_sync();
     STAMP(7);
 
-    /* ---- phase 3: mass-matrix entries and right-hand side, fixed-order sums */
+    /* ---- phase 3: right-hand side and mass-matrix entries, fixed-order sums.
+     * 3a (lane = dof d): rhs_d = -S_d.WB + muscle/actuator torques + contact
+     * J_d(s).F_s + limits; for the implicit step also the per-foot vectors
+     * Y_{b,d} = sum_{s on b} (P_s x w, w), w = C_s J_d(s), so that the
+     * implicit contact block of an entry is sum_b S_l . Y_{b,k} (six FMAs per
+     * foot instead of a Jacobian pair and a 3x3 form per sphere).
+     * 3b: Y to LDS (over the consumed torque slots).  3c (lane = entry):
+     * composite-rigid-body M entries + implicit contact and limit terms. */
+    using FT = Feet<T>;
+    const bool implicit = h > 0;
+    if (lane < ND) {
+        const Real *Sd = lds + LY::S + 6 * lane, *wb = lds + LY::WB + 6 * SM.dof_cb[lane];
+        Real r = -(dot3(Sd, wb) + dot3(Sd + 3, wb + 3));
+#pragma unroll
+        for (int m = 0; m < LY::NTL; ++m) r += lds[LY::TAU + ND * m + lane];
+        Real Y[FT::N > 0 ? FT::N : 1][6];
+#pragma unroll
+        for (int b = 0; b < FT::N; ++b)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) Y[b][i] = 0;
+        sfor<0, T::NS>([&](auto sI) {
+            constexpr int sp = decltype(sI)::value;
+            constexpr unsigned msk = T::dofmask[T::sphere_cb[sp]];
+            const Real *cj = lds + LY::CJ + LY::CJN * sp, *C = cj + 6;
+            Real jd[3];
+            contact_jac(Sd, cj, jd);
+            const bool on = lds[LY::CW + 8 * sp + 6] > 0 && ((msk >> lane) & 1u);
+            r += on ? dot3(jd, cj + 3) : Real(0);
+            if (implicit) {
+                Real w[3] = {C[0] * jd[0] + C[1] * jd[2], C[2] * jd[1], C[1] * jd[0] + C[3] * jd[2]};
+                Real pw[3];
+                cross3(cj, w, pw);
+                constexpr int fb = FT::of(sp);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    Y[fb][i] += on ? pw[i] : Real(0);
+                    Y[fb][3 + i] += on ? w[i] : Real(0);
+                }
+            }
+        });
+#pragma unroll
+        for (int li = 0; li < T::NL; ++li)
+            if (SM.lim_dof[li] == lane) r += lds[LY::LIM + 4 * li + 2];
+        lds[LY::RHS + lane] = r;
+        if (implicit) {
+            wave_sync_lanes();   /* every dof lane has read the torque slots */
+#pragma unroll
+            for (int b = 0; b < FT::N; ++b)
+#pragma unroll
+                for (int i = 0; i < 6; ++i) lds[LY::TAU + 6 * (ND * b + lane) + i] = Y[b][i];
+        }
+    }
+    wave_sync();
     for (int e = lane; e < NP; e += G) {
         int l = SM.e_l[e], k = SM.e_k[e], c = SM.e_c[e];
         const Real *Sl = lds + LY::S + 6 * l, *Sk = lds + LY::S + 6 * k;
@@ -1232,46 +1322,21 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
             for (int i = 0; i < 3; ++i) Pm[i] = ic[0] * Sl[3 + i] + t[i];
             v = dot3(Sk, Lm) + dot3(Sk + 3, Pm);
         }
-        if (h > 0) {
-            /* implicit contact: J_l.C J_k per sphere whose body both dofs move;
-             * every slot is read (independent loads), inactive spheres (stale
-             * slots) are dropped by a select */
-            sfor<0, T::NS>([&](auto sI) {
-                constexpr int sp = decltype(sI)::value;
-                constexpr unsigned msk = T::dofmask[T::sphere_cb[sp]];
-                const Real *cj = lds + LY::CJ + LY::CJN * sp, *C = cj + 6;
-                Real jl[3], jk[3];
-                contact_jac(Sl, cj, jl);
-                contact_jac(Sk, cj, jk);
-                Real term = jl[0] * (C[0] * jk[0] + C[1] * jk[2]) + jl[1] * (C[2] * jk[1]) + jl[2] * (C[1] * jk[0] + C[3] * jk[2]);
-                const bool on = lds[LY::CW + 8 * sp + 6] > 0 && ((msk >> l) & (msk >> k) & 1u);
-                v += on ? term : Real(0);
-            });
+        if (implicit) {
+            /* implicit contact: S_l . Y_{b,k} for each foot b both dofs move */
+#pragma unroll
+            for (int b = 0; b < FT::N; ++b) {
+                const unsigned msk = T::dofmask[FT::cb(b)];
+                const Real *y = lds + LY::TAU + 6 * (ND * b + k);
+                const Real term = dot3(Sl, y) + dot3(Sl + 3, y + 3);
+                v += ((msk >> l) & (msk >> k) & 1u) ? term : Real(0);
+            }
             if (l == k)
 #pragma unroll
                 for (int li = 0; li < T::NL; ++li)
                     if (SM.lim_dof[li] == l) v += lds[LY::LIM + 4 * li + 1];
         }
         lds[LY::MP + e] = v;
-    }
-    if (lane < ND) {
-        const Real *Sd = lds + LY::S + 6 * lane, *wb = lds + LY::WB + 6 * SM.dof_cb[lane];
-        Real r = -(dot3(Sd, wb) + dot3(Sd + 3, wb + 3));
-#pragma unroll
-        for (int m = 0; m < LY::NTL; ++m) r += lds[LY::TAU + ND * m + lane];
-        sfor<0, T::NS>([&](auto sI) {
-            constexpr int sp = decltype(sI)::value;
-            constexpr unsigned msk = T::dofmask[T::sphere_cb[sp]];
-            const Real *cj = lds + LY::CJ + LY::CJN * sp;
-            Real jd[3];
-            contact_jac(Sd, cj, jd);
-            const Real term = dot3(jd, cj + 3);
-            r += (lds[LY::CW + 8 * sp + 6] > 0 && ((msk >> lane) & 1u)) ? term : Real(0);
-        });
-#pragma unroll
-        for (int li = 0; li < T::NL; ++li)
-            if (SM.lim_dof[li] == lane) r += lds[LY::LIM + 4 * li + 2];
-        lds[LY::RHS + lane] = r;
     }
     wave_sync();
     STAMP(8);
