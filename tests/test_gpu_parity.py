@@ -367,3 +367,45 @@ def test_perturbation_config_sharded():
         assert torch.equal(o, o2), t
     for e in [full] + parts:
         e.close()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+@pytest.mark.parametrize('env_id', ['MuscleWalkingImitation2D-v0', 'TorqueWalkingImitation2D-v0',
+                                    'MuscleRunningImitation3D-v0'])
+def test_parity_200_identical_action_steps(env_id):
+    """north_star / SURVEY 8d parity run: 200 identical-action steps per env,
+    no auto-reset, masked after done; observations and rewards within 1e-4
+    relative (fp64 GPU vs the fp64 oracle).  Actions are mild (muscle
+    excitations U[0, 0.4]; PD targets at the reference plus N(0, 0.02)) so
+    that a good share of the envs stays up for the whole run."""
+    import torch
+    rng = np.random.default_rng(200)
+    n, T = 24, 200
+    pk, env, orc, bufs = _setup(env_id, n, 64)
+    rows = rng.integers(0, min(pk.reset_hi, pk.n_episode - T) + 1, size=n)
+    env.reset(ref_index=rows)
+    for i in range(n):
+        orc.reset(bufs, i, int(rows[i]))
+    alive = np.ones(n, bool)
+    worst, lived = 0.0, np.zeros(n, int)
+    for t in range(T):
+        if 'Muscle' in env_id:
+            acts = rng.uniform(0.0, 0.4, size=(n, env.action_dim))
+        else:
+            st = np.array([orc.get_state(bufs, i)[1] for i in range(n)]).astype(int) + 1
+            acts = np.array([[pk.ref_q[min(r, pk.nrows - 1)][pk.pd_coord[a]] for a in range(env.action_dim)]
+                             for r in st]) + rng.normal(0.0, 0.02, size=(n, env.action_dim))
+        obs, rew, done, info = env.step(torch.as_tensor(acts, device=env.device))
+        torch.cuda.synchronize()
+        obs, rew, done = (v.cpu().numpy() for v in (obs, rew, done))
+        for i in np.where(alive)[0]:
+            o, r, d, _ = orc.step(bufs, i, acts[i])
+            e = max(_rel(obs[i], o).max(), abs(rew[i] - r) / max(1.0, abs(r)))
+            assert e < 1e-4, (t, i, e)
+            assert bool(done[i]) == d, (t, i)
+            worst = max(worst, e)
+            lived[i] += 1
+            alive[i] = not d
+    print(f'{env_id} 200-step parity: max rel err {worst:.2e}; steps lived min/median/max '
+          f'{lived.min()}/{int(np.median(lived))}/{lived.max()}, alive at the end {alive.sum()}/{n}')
+    env.close()
