@@ -52,7 +52,7 @@ struct DPathPt {
     int32_t type, cbody, cond_coord, mcoord; /* mcoord: moving point coordinate (-1 none) */
     int32_t mdof;                             /* its dof (-1 locked/none)                 */
     uint32_t dofmask;                         /* dofs moving this point                   */
-    int32_t fn[3];
+    int32_t mf[3];                            /* moving point: slot of each axis' function (-1: loc) */
     int32_t pad;
     Real loc[3], R[9], p[3];
     Real lo, hi;
@@ -130,6 +130,9 @@ struct SModel {
     int32_t coord_dof[D::NCD], dof_cb[D::NDD], dof_coord[D::NDD];
     int32_t e_l[D::NP], e_k[D::NP], e_c[D::NP]; /* packed-lower M entry -> (row, col, subtree body) */
     uint32_t dofmask[T::NB];
+    /* moving-point location functions: evaluated lane-parallel once per
+     * dynamics call into the env's MF slots (function index, coordinate) */
+    int32_t mf_fn[T::NMF > 0 ? T::NMF : 1], mf_coord[T::NMF > 0 ? T::NMF : 1];
     /* OpenSim bodies reported in observations / rewards (lane = body) */
     Real os_p[T::NOS][3];
     int32_t os_cb[T::NOS];

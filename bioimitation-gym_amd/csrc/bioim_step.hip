@@ -381,7 +381,8 @@ template <class T, typename Real> struct Lay {
     static constexpr int RHS = MP + NP;          /* [ND]                                            */
     static constexpr int CW = RHS + ND;          /* [NS][8]: F3, Mo3, active                        */
     static constexpr int LIM = CW + 8 * NS;      /* [NL][4]: f, diag add, tau add                   */
-    static constexpr int U = ((LIM + 4 * NL + 1) / 2) * 2;
+    static constexpr int MF = LIM + 4 * NL;      /* [NMF][2]: moving-point functions f, df/dq       */
+    static constexpr int U = ((MF + 2 * (T::NMF > 0 ? T::NMF : 1) + 1) / 2) * 2;
     static constexpr int LOC = U;                /* phase 1: [NB+1][24] joint-local data (NB: identity) */
     static constexpr int SL = LOC + 24 * (NB + 1); /* phase 1: [ND][6] joint-local Plucker columns  */
     static constexpr int TAU = U;                /* phases 2-3: [NTL][ND] per-lane muscle/actuator torques */
@@ -1019,10 +1020,9 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
                         Real ll[3], dl[3] = {0, 0, 0};
 #pragma unroll
                         for (int a = 0; a < 3; ++a) {
-                            Real f, f1, f2;
-                            fn_eval<T, Real>(SM, pt.fn[a], ldsq[pt.mcoord], f, f1, f2);
-                            ll[a] = pt.fn[a] < 0 ? pt.loc[a] : f;
-                            dl[a] = pt.fn[a] < 0 ? Real(0) : f1;
+                            const int f = pt.mf[a];
+                            ll[a] = f < 0 ? pt.loc[a] : lds[LY::MF + 2 * (f < 0 ? 0 : f)];
+                            dl[a] = f < 0 ? Real(0) : lds[LY::MF + 2 * (f < 0 ? 0 : f) + 1];
                         }
                         mv3(pt.R, ll, loc);
 #pragma unroll
@@ -1124,6 +1124,16 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     /* ---- phase 1: lane-parallel kinematics */
     if (lane < NB) kin_local<T, Real>(SM, lds, lane);
     if (lane == NB) kin_ground<T, Real>(lds, x0);
+    if constexpr (T::NMF > 0) {
+        /* moving path points' location functions of their coordinate, one
+         * lane each (read by every muscle that has the point) */
+        for (int f = lane; f < T::NMF; f += G) {
+            Real v, d1, d2;
+            fn_eval<T, Real>(SM, SM.mf_fn[f], lds[LY::QF + SM.mf_coord[f]], v, d1, d2);
+            lds[LY::MF + 2 * f] = v;
+            lds[LY::MF + 2 * f + 1] = d1;
+        }
+    }
     wave_sync();
     STAMP(0);
     if (lane < NB) kin_chain<T, Real>(SM, lds, lane, x0);
@@ -2238,16 +2248,23 @@ template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, 
     }
     std::vector<uint32_t> dofmask(T::NB, 0);
     for (int c = 0; c < T::NB; ++c) dofmask[c] = T::dofmask[c];
+    int nmf = 0;
     for (int j = 0; j < p.npathpt; ++j) {
         const bioim_pathpt_t &s = p.pathpt[j];
         DPathPt<Real> &d = m.pt[j];
         d.type = s.type; d.cbody = s.cbody; d.cond_coord = s.cond_coord;
         d.mcoord = -1; d.mdof = -1;
         for (int a = 0; a < 3; ++a) {
-            d.fn[a] = s.fn[a];
+            d.mf[a] = -1;
             if (s.type == BIOIM_PT_MOVING && s.fn[a] >= 0) {
                 d.mcoord = p.fn[s.fn[a]].coord;
                 d.mdof = d.mcoord >= 0 ? p.coord[d.mcoord].dof : -1;
+                if (nmf < T::NMF) {
+                    m.mf_fn[nmf] = s.fn[a];
+                    m.mf_coord[nmf] = p.fn[s.fn[a]].coord;
+                    d.mf[a] = nmf;
+                }
+                ++nmf;
             }
         }
         d.dofmask = dofmask[s.cbody];
@@ -2332,6 +2349,19 @@ template <class T> bool topology_matches(const bioim_modelpack_t &p) {
         return false;
     if (p.coord_tx != T::TX || p.coord_ty != T::TY || p.coord_tz != T::TZ) return false;
     if (p.npathpt != T::NPT || p.nfn != T::NFN || p.nknots != T::NKNOT) return false;
+    {   /* moving-point function slots and muscle spans fit the compiled sizes */
+        int nmf = 0;
+        for (int j = 0; j < p.npathpt; ++j)
+            for (int a = 0; a < 3; ++a) nmf += (p.pathpt[j].type == BIOIM_PT_MOVING && p.pathpt[j].fn[a] >= 0) ? 1 : 0;
+        if (nmf != T::NMF) return false;
+        uint32_t root = ~0u;
+        for (int c = 0; c < T::NB; ++c) root &= T::dofmask[c];
+        for (int i = 0; i < p.nmuscle; ++i) {
+            uint32_t u = 0;
+            for (int j = 0; j < p.muscle[i].npt; ++j) u |= T::dofmask[p.pathpt[p.muscle[i].pt_off + j].cbody];
+            if (__builtin_popcount(u & ~root) > T::MAXSPAN || T::MAXSPAN > BIOIM_MAX_SPAN) return false;
+        }
+    }
     for (int f = 0; f < p.nfn; ++f)
         if (p.fn[f].nknots > T::NKMAX) return false;
     if ((int)unique_curves(p, nullptr).size() != T::NCURVE) return false;

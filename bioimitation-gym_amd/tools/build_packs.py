@@ -161,6 +161,8 @@ def emit_topology(struct, pk, lanes):
         maxspan = max(maxspan, bin(u & ~root).count('1'))
     s += f'    static constexpr int MAXPT = {maxpt}; /* path points per muscle (max) */\n'
     s += f'    static constexpr int MAXSPAN = {maxspan}; /* non-root dofs a muscle path moves (max) */\n'
+    nmf = sum(1 for j in range(pk.npathpt) if pk.pathpt[j].type == 2 for a in range(3) if pk.pathpt[j].fn[a] >= 0)
+    s += f'    static constexpr int NMF = {nmf}; /* moving-point location functions (one lane each, per dynamics call) */\n'
     s += f'    static constexpr unsigned PT_COND = {cond}u, PT_MOVING = {move}u; /* point indices that can be conditional / moving */\n'
     s += f'    static constexpr int TX = {pk.coord_tx}, TY = {pk.coord_ty}, TZ = {pk.coord_tz};\n'
     s += f'    static constexpr int TORSO = {pk.torso_body}, CALCN_R = {pk.calcn_r_body}, CALCN_L = {pk.calcn_l_body};\n'
