@@ -65,6 +65,7 @@ struct SBody {
     Real axis[6][3];
     Real mass, com[3], inertia[6];
     int32_t fn[6];          /* function per spatial-transform axis (-1 none)      */
+    int32_t js[6];          /* its function slot if a spline (-1 otherwise)       */
     int32_t parent, pslot;  /* tree parent (-1 ground); its frame slot (ground NB) */
 };
 
@@ -90,6 +91,16 @@ template <class T> struct TopoInfo {
         for (int c = 0; c < T::NB; ++c) m |= 1u << (T::axis_kind[c * 6 + a] + 1);
         return m;
     }
+    /* (body, axis) pairs whose function is a spline: evaluated lane-parallel
+     * before the joint kinematics, like the moving-point functions */
+    static constexpr int njs() {
+        int n = 0;
+        for (int c = 0; c < T::NB; ++c)
+            for (int a = 0; a < 6; ++a) n += T::axis_kind[c * 6 + a] == BIOIM_FN_SPLINE ? 1 : 0;
+        return n;
+    }
+    /* function slots per dynamics call: moving-point functions, then joint splines */
+    static constexpr int nslot() { return T::NMF + njs(); }
     static constexpr int depth_of(int c) {
         int l = 1;
         for (int p = T::parent[c]; p >= 0; p = T::parent[p]) ++l;
@@ -132,7 +143,8 @@ struct SModel {
     uint32_t dofmask[T::NB];
     /* moving-point location functions: evaluated lane-parallel once per
      * dynamics call into the env's MF slots (function index, coordinate) */
-    int32_t mf_fn[T::NMF > 0 ? T::NMF : 1], mf_coord[T::NMF > 0 ? T::NMF : 1];
+    int32_t mf_fn[TopoInfo<T>::nslot() > 0 ? TopoInfo<T>::nslot() : 1];
+    int32_t mf_coord[TopoInfo<T>::nslot() > 0 ? TopoInfo<T>::nslot() : 1];
     /* OpenSim bodies reported in observations / rewards (lane = body) */
     Real os_p[T::NOS][3];
     int32_t os_cb[T::NOS];

@@ -381,8 +381,9 @@ template <class T, typename Real> struct Lay {
     static constexpr int RHS = MP + NP;          /* [ND]                                            */
     static constexpr int CW = RHS + ND;          /* [NS][8]: F3, Mo3, active                        */
     static constexpr int LIM = CW + 8 * NS;      /* [NL][4]: f, diag add, tau add                   */
-    static constexpr int MF = LIM + 4 * NL;      /* [NMF][2]: moving-point functions f, df/dq       */
-    static constexpr int U = ((MF + 2 * (T::NMF > 0 ? T::NMF : 1) + 1) / 2) * 2;
+    static constexpr int NSLOT = TopoInfo<T>::nslot();
+    static constexpr int MF = LIM + 4 * NL;      /* [NSLOT][3]: function slots f, f', f''           */
+    static constexpr int U = ((MF + 3 * (NSLOT > 0 ? NSLOT : 1) + 1) / 2) * 2;
     static constexpr int LOC = U;                /* phase 1: [NB+1][24] joint-local data (NB: identity) */
     static constexpr int SL = LOC + 24 * (NB + 1); /* phase 1: [ND][6] joint-local Plucker columns  */
     static constexpr int TAU = U;                /* phases 2-3: [NTL][ND] per-lane muscle/actuator torques */
@@ -478,7 +479,13 @@ DEV void kin_local(const SModel<T, Real> &SM, Real *lds, int c) {
             qc = cc >= 0 ? qc : Real(0);
             uc = cc >= 0 ? uc : Real(0);
             Real f, f1, f2;
-            fn_eval_km<KM, T, Real>(SM, fi, qc, f, f1, f2);
+            fn_eval_km<KM & ~(1u << (BIOIM_FN_SPLINE + 1)), T, Real>(SM, fi, qc, f, f1, f2);
+            if constexpr ((KM & (1u << (BIOIM_FN_SPLINE + 1))) != 0) {
+                const int js = b.js[ax];   /* spline axes: evaluated in phase 0b */
+                if (js >= 0) {
+                    f = lds[LY::MF + 3 * js]; f1 = lds[LY::MF + 3 * js + 1]; f2 = lds[LY::MF + 3 * js + 2];
+                }
+            }
             cd[ax] = cc >= 0 ? SM.coord_dof[cs] : -1;
             Real a[3] = {b.axis[ax][0], b.axis[ax][1], b.axis[ax][2]};
             if constexpr (ax < 3) {
@@ -650,6 +657,24 @@ DEV void kin_chain(const SModel<T, Real> &SM, Real *lds, int c, Real x0) {
     for (int i = 0; i < 3; ++i) {
         kb[9 + i] = F.o[i]; kb[12 + i] = F.w[i]; kb[15 + i] = F.vO[i];
         ab[i] = F.al[i]; ab[3 + i] = F.aO[i];
+    }
+}
+
+/* Phase 0b: the function slots (Lay::MF), one lane each — moving path
+ * points' location functions and the joints' spline axes — from the
+ * published coordinates; ends with a wave sync when there are any */
+template <class T, typename Real>
+DEV void fn_slots(const SModel<T, Real> &SM, Real *lds, int lane) {
+    using LY = Lay<T, Real>;
+    if constexpr (LY::NSLOT > 0) {
+        for (int f = lane; f < LY::NSLOT; f += T::G) {
+            Real v, d1, d2;
+            fn_eval<T, Real>(SM, SM.mf_fn[f], lds[LY::QF + SM.mf_coord[f]], v, d1, d2);
+            lds[LY::MF + 3 * f] = v;
+            lds[LY::MF + 3 * f + 1] = d1;
+            lds[LY::MF + 3 * f + 2] = d2;
+        }
+        wave_sync();
     }
 }
 
@@ -1021,8 +1046,8 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
 #pragma unroll
                         for (int a = 0; a < 3; ++a) {
                             const int f = pt.mf[a];
-                            ll[a] = f < 0 ? pt.loc[a] : lds[LY::MF + 2 * (f < 0 ? 0 : f)];
-                            dl[a] = f < 0 ? Real(0) : lds[LY::MF + 2 * (f < 0 ? 0 : f) + 1];
+                            ll[a] = f < 0 ? pt.loc[a] : lds[LY::MF + 3 * (f < 0 ? 0 : f)];
+                            dl[a] = f < 0 ? Real(0) : lds[LY::MF + 3 * (f < 0 ? 0 : f) + 1];
                         }
                         mv3(pt.R, ll, loc);
 #pragma unroll
@@ -1121,19 +1146,14 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     }
     D.x0 = x0;
 
+    /* ---- phase 0b: function slots, one lane each — the moving path points'
+     * location functions (read by every muscle that has the point) and the
+     * joints' spline axes (read by their body's lane) */
+    fn_slots<T, Real>(SM, lds, lane);
+
     /* ---- phase 1: lane-parallel kinematics */
     if (lane < NB) kin_local<T, Real>(SM, lds, lane);
     if (lane == NB) kin_ground<T, Real>(lds, x0);
-    if constexpr (T::NMF > 0) {
-        /* moving path points' location functions of their coordinate, one
-         * lane each (read by every muscle that has the point) */
-        for (int f = lane; f < T::NMF; f += G) {
-            Real v, d1, d2;
-            fn_eval<T, Real>(SM, SM.mf_fn[f], lds[LY::QF + SM.mf_coord[f]], v, d1, d2);
-            lds[LY::MF + 2 * f] = v;
-            lds[LY::MF + 2 * f + 1] = d1;
-        }
-    }
     wave_sync();
     STAMP(0);
     if (lane < NB) kin_chain<T, Real>(SM, lds, lane, x0);
@@ -1498,6 +1518,7 @@ __global__ __launch_bounds__(BIOIM_WG) void id_kernel(IdArgs<T, Real> a) {
     if constexpr (T::TX >= 0) {
         if constexpr (T::coord_dof[T::TX] >= 0) x0 = M.float_origin ? lds[LY::QF + T::TX] : Real(0);
     }
+    fn_slots<T, Real>(SM, lds, lane);
     if (lane < NB) kin_local<T, Real>(SM, lds, lane);
     if (lane == NB) kin_ground<T, Real>(lds, x0);
     wave_sync();
@@ -2272,9 +2293,19 @@ template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, 
         for (int i = 0; i < 9; ++i) d.R[i] = (Real)s.R[i];
         d.lo = (Real)s.range_lo; d.hi = (Real)s.range_hi;
     }
+    int jslot = T::NMF;   /* joint spline slots follow the moving-point ones */
     for (int c = 0; c < p.ncbody; ++c) {
         const bioim_cbody_t &b = p.cbody[c];
         SBody<Real> &d = m.body[c];
+        for (int a = 0; a < 6; ++a) {
+            d.js[a] = -1;
+            const int fi = p.cbody[c].fn[a];
+            if (fi >= 0 && p.fn[fi].type == BIOIM_FN_SPLINE && jslot < TopoInfo<T>::nslot()) {
+                m.mf_fn[jslot] = fi;
+                m.mf_coord[jslot] = p.fn[fi].coord;
+                d.js[a] = jslot++;
+            }
+        }
         for (int i = 0; i < 9; ++i) { d.R_pf[i] = (Real)b.R_pf[i]; d.R_mb[i] = (Real)b.R_mb[i]; }
         for (int i = 0; i < 3; ++i) { d.p_pf[i] = (Real)b.p_pf[i]; d.p_mb[i] = (Real)b.p_mb[i]; d.com[i] = (Real)b.com[i]; }
         for (int a = 0; a < 6; ++a) {
