@@ -214,6 +214,15 @@ DEV void sincos_rt(double x, double &s, double &c) {
 DEV void sincos_rt(float x, float &s, float &c) { sincosf(x, &s, &c); }
 
 /* ----------------------------------------------------- smooth curves */
+/* reciprocal for Newton updates (a self-correcting iteration tolerates a
+ * last-bits error in the step): hardware rcp plus one refinement */
+DEV double newton_rcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    const double e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+DEV float newton_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
 /* a quintic segment in the power basis c[0] + c[1] u + ... + c[5] u^5
  * (converted from the Bezier control points at create time, convert_curve):
  * Horner, 5 FMAs; the derivative 4 */
@@ -244,7 +253,7 @@ DEV void curve_eval(const DCurve<Real> &C, Real x, Real &y, Real &dydx) {
     Real fr = tt - Real(i0);
     Real u = C.ut[k][i0] + fr * (C.ut[k][i0 + 1] - C.ut[k][i0]);
 #pragma unroll
-    for (int it = 0; it < 3; ++it) u -= (bez5(px, u) - xc) / dbez5(px, u);
+    for (int it = 0; it < 3; ++it) u -= (bez5(px, u) - xc) * newton_rcp(dbez5(px, u));
     y = bez5(py, u);
     dydx = dbez5(py, u) / dbez5(px, u);
     if (x < C.x0) { y = C.y0 + C.dydx0 * (x - C.x0); dydx = C.dydx0; }
@@ -289,7 +298,7 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
         Real g = bez5(pg, u);
         if (g > 0) hi = u; else lo = u;
         Real dg = dbez5(pg, u);
-        Real un = u - g / dg;
+        Real un = u - g * newton_rcp(dg);
         /* inclusive bracket: a converged step (un == u == lo or hi after
          * rounding) must not trigger the bisection fallback */
         if (!(un >= lo && un <= hi)) un = Real(0.5) * (lo + hi);
@@ -759,9 +768,12 @@ template <typename Real> DEV void symv(const Real *J, const Real *v, Real *o) {
     o[0] = x; o[1] = y; o[2] = z;
 }
 
-/* in-place packed-lower Cholesky solve; returns false if not SPD */
+/* in-place packed-lower Cholesky solve; returns false if not SPD.  One
+ * reciprocal per column, reused by both substitutions (divisions sit on the
+ * solve's critical path) */
 template <int N, typename Real> DEV bool cholesky_solve(Real *A, Real *b) {
     bool ok = true;
+    Real inv[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         Real s = A[tri<0>(j, j)];
@@ -769,14 +781,14 @@ template <int N, typename Real> DEV bool cholesky_solve(Real *A, Real *b) {
         for (int k = 0; k < j; ++k) s -= A[tri<0>(j, k)] * A[tri<0>(j, k)];
         ok = ok && (s > 0);
         Real d = sqrt(s > 0 ? s : Real(1e-30));
-        Real inv = Real(1) / d;
+        inv[j] = Real(1) / d;
         A[tri<0>(j, j)] = d;
 #pragma unroll
         for (int i = j + 1; i < N; ++i) {
             Real t = A[tri<0>(i, j)];
 #pragma unroll
             for (int k = 0; k < j; ++k) t -= A[tri<0>(i, k)] * A[tri<0>(j, k)];
-            A[tri<0>(i, j)] = t * inv;
+            A[tri<0>(i, j)] = t * inv[j];
         }
     }
 #pragma unroll
@@ -784,14 +796,14 @@ template <int N, typename Real> DEV bool cholesky_solve(Real *A, Real *b) {
         Real t = b[i];
 #pragma unroll
         for (int k = 0; k < i; ++k) t -= A[tri<0>(i, k)] * b[k];
-        b[i] = t / A[tri<0>(i, i)];
+        b[i] = t * inv[i];
     }
 #pragma unroll
     for (int i = N - 1; i >= 0; --i) {
         Real t = b[i];
 #pragma unroll
         for (int k = i + 1; k < N; ++k) t -= A[tri<0>(k, i)] * b[k];
-        b[i] = t / A[tri<0>(i, i)];
+        b[i] = t * inv[i];
     }
     return ok;
 }
