@@ -222,6 +222,21 @@ DEV double newton_rcp(double x) {
     return fma(r, e, r);
 }
 DEV float newton_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+/* reciprocal to (about) the last bit: hardware rcp plus two refinements —
+ * a shorter dependency chain than the IEEE division sequence; used where the
+ * divisor is a well-scaled positive quantity (lengths, cosines, time
+ * constants, slip speeds) */
+DEV double fast_rcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+DEV float fast_rcp(float x) {
+    float r = __builtin_amdgcn_rcpf(x);
+    return fmaf(r, fmaf(-x, r, 1.0f), r);
+}
 
 /* a quintic segment in the power basis c[0] + c[1] u + ... + c[5] u^5
  * (converted from the Bezier control points at create time, convert_curve):
@@ -255,7 +270,7 @@ DEV void curve_eval(const DCurve<Real> &C, Real x, Real &y, Real &dydx) {
 #pragma unroll
     for (int it = 0; it < 3; ++it) u -= (bez5(px, u) - xc) * newton_rcp(dbez5(px, u));
     y = bez5(py, u);
-    dydx = dbez5(py, u) / dbez5(px, u);
+    dydx = dbez5(py, u) * fast_rcp(dbez5(px, u));
     if (x < C.x0) { y = C.y0 + C.dydx0 * (x - C.x0); dydx = C.dydx0; }
     if (x > C.x1) { y = C.y1 + C.dydx1 * (x - C.x1); dydx = C.dydx1; }
 }
@@ -319,7 +334,7 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
     }
     v = bez5(px, u);
     fv = bez5(py, u);
-    dfv = dbez5(py, u) / dbez5(px, u);
+    dfv = dbez5(py, u) * fast_rcp(dbez5(px, u));
     if (g0 >= 0) {
         v = (rhs - afal * (C.y0 - C.dydx0 * C.x0)) / (afal * C.dydx0 + beta);
         fv = C.y0 + C.dydx0 * (v - C.x0); dfv = C.dydx0;
@@ -864,17 +879,19 @@ DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, int s, Real h) {
     Real vt0 = -vs[0], vt2 = -vs[2];
     Real vslip = sqrt(vt0 * vt0 + vt2 * vt2);
     Real vtr = SM.cf_vt[fo], ms = SM.cf_ms[fo], md = SM.cf_md[fo], mv = SM.cf_mv[fo];
-    Real r_ = vslip / vtr, den = Real(1) + r_ * r_;
+    const Real ivtr = fast_rcp(vtr);
+    Real r_ = vslip * ivtr, den = Real(1) + r_ * r_;
+    const Real iden = fast_rcp(den), ivs = vslip > 0 ? fast_rcp(vslip) : Real(0);
     if (vslip != 0) {
-        Real ff = fn * (fmin(r_, Real(1)) * (md + Real(2) * (ms - md) / den) + mv * vslip);
-        F[0] += ff * vt0 / vslip;
-        F[2] += ff * vt2 / vslip;
+        Real ff = fn * (fmin(r_, Real(1)) * (md + Real(2) * (ms - md) * iden) + mv * vslip);
+        F[0] += ff * vt0 * ivs;
+        F[2] += ff * vt2 * ivs;
     }
     Real mo[3];
     cross3(P, F, mo);
 #pragma unroll
     for (int i = 0; i < 3; ++i) { cw[i] = F[i]; cw[3 + i] = mo[i]; }
-    Real kn = Real(1.5) * fH / depth * (Real(1) + Real(1.5) * SM.cf_c[fo] * vn);
+    Real kn = Real(1.5) * fH * fast_rcp(depth) * (Real(1) + Real(1.5) * SM.cf_c[fo] * vn);
     /* implicit extra force -h*Kn*v_y (Hertz force at the advanced position) */
 #pragma unroll
     for (int i = 0; i < 3; ++i) cj[i] = P[i];
@@ -885,15 +902,15 @@ DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, int s, Real h) {
     if (h > 0) {
         Real g_s, gp;
         if (r_ < 1) {
-            g_s = (md + Real(2) * (ms - md) / den) / vtr + mv;
-            gp = (md + Real(2) * (ms - md) / den) / vtr - Real(4) * (ms - md) * r_ * r_ / (den * den * vtr) + mv;
+            g_s = (md + Real(2) * (ms - md) * iden) * ivtr + mv;
+            gp = (md + Real(2) * (ms - md) * iden) * ivtr - Real(4) * (ms - md) * r_ * r_ * (iden * iden * ivtr) + mv;
         } else {
-            g_s = (md + Real(2) * (ms - md) / den) / vslip + mv;
-            gp = -Real(4) * (ms - md) * r_ / (den * den * vtr) + mv;
+            g_s = (md + Real(2) * (ms - md) * iden) * ivs + mv;
+            gp = -Real(4) * (ms - md) * r_ * (iden * iden * ivtr) + mv;
         }
         gp = gp < 0 ? Real(0) : gp;
         Real tx = 0, tz = 0;
-        if (vslip > 0) { tx = vt0 / vslip; tz = vt2 / vslip; }
+        if (vslip > 0) { tx = vt0 * ivs; tz = vt2 * ivs; }
         Real ctt = h * fn * g_s, cq = h * fn * (gp - g_s);
         cyy = h * Real(1.5) * SM.cf_c[fo] * fH + h * h * kn;
         cxx = ctt + cq * tx * tx;
@@ -925,13 +942,14 @@ DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_
     Real lce = l_state < mu.lmin ? mu.lmin : l_state;
     Real w = mu.width;
     Real sq = sqrt(lce * lce - w * w);
-    Real cosphi = sq / lce;
+    const Real isq = fast_rcp(sq);
+    const Real icos = lce * isq;          /* 1 / cos(pennation) */
     Real lt = L - sq;
     Real fse, dfse, fal, dfal, fpe, dfpe;
     curve_eval(Cfse, lt * mu.inv_lts, fse, dfse);
     curve_eval(Cfal, lce * mu.inv_lopt, fal, dfal);
     curve_eval(Cfpe, lce * mu.inv_lopt, fpe, dfpe);
-    Real rhs = fse / cosphi - fpe;
+    Real rhs = fse * icos - fpe;
     Real vN, fvv, dfv;
     solve_fv(Cfv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
     Real dGdv = a * fal * dfv + mu.beta;
@@ -950,11 +968,12 @@ DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_
     s.Fa = mu.fiso * a * fal * fvv;
     s.Ff = mu.fiso * (a * fal * fvv + fpe + mu.beta * vN);
     s.clamped = clamped;
-    Real dGdl = (a * dfal * fvv + dfpe) * mu.inv_lopt + dfse * mu.inv_lts / (cosphi * cosphi) + fse * w * w / (sq * sq * sq);
-    s.dvdl = clamped ? Real(0) : -(dGdl / dGdv) * mu.lv;
+    Real dGdl = (a * dfal * fvv + dfpe) * mu.inv_lopt + dfse * mu.inv_lts * (icos * icos) + fse * w * w * (isq * isq * isq);
+    s.dvdl = clamped ? Real(0) : -(dGdl * fast_rcp(dGdv)) * mu.lv;
     Real u = excitation < mu.amin ? mu.amin : (excitation > Real(1) ? Real(1) : excitation);
-    Real tau = u > a ? mu.tau_act * (Real(0.5) + Real(1.5) * a) : mu.tau_deact / (Real(0.5) + Real(1.5) * a);
-    s.dadt = (u - a) / tau;
+    const Real ab = Real(0.5) + Real(1.5) * a;
+    /* du/dt = (u - a) / tau, tau = tau_act (0.5 + 1.5 a) or tau_deact / (0.5 + 1.5 a) */
+    s.dadt = u > a ? (u - a) * fast_rcp(mu.tau_act * ab) : (u - a) * ab * fast_rcp(mu.tau_deact);
 }
 
 /* static fiber equilibrium at reset (zero fiber velocity) */
@@ -1078,7 +1097,7 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
                     Real sgm[3] = {P[0] - Pp[0], P[1] - Pp[1], P[2] - Pp[2]};
                     Real len = sqrt(dot3(sgm, sgm));
                     L += len;
-                    Real inv = Real(1) / len;
+                    Real inv = fast_rcp(len);
 #pragma unroll
                     for (int a = 0; a < 3; ++a) e[a] = sgm[a] * inv;
                     Real g[3] = {ep[0] - e[0], ep[1] - e[1], ep[2] - e[2]};
