@@ -139,7 +139,9 @@ struct SModel {
     Real ca_opt[D::NAD], ca_min[D::NAD], ca_max[D::NAD], kp[D::NAD], kv[D::NAD];
     /* index tables */
     int32_t coord_dof[D::NCD], dof_cb[D::NDD], dof_coord[D::NDD];
-    int32_t e_l[D::NP], e_k[D::NP], e_c[D::NP]; /* packed-lower M entry -> (row, col, subtree body) */
+    /* packed-lower M entry e -> bytes (row l, col k, deeper dof dp (0xff:
+     * different branches, M_lk = 0), the other dof) */
+    uint32_t e_pk[D::NP];
     uint32_t dofmask[T::NB];
     /* moving-point location functions: evaluated lane-parallel once per
      * dynamics call into the env's MF slots (function index, coordinate) */

@@ -415,7 +415,8 @@ template <class T, typename Real> struct Lay {
     static constexpr int OBS = U;                /* report: observation staging                     */
     static constexpr int REP = OBS + OBSMAX;     /* report: [NOS+1][6] body pos/vel (NOS: COM)      */
     static constexpr int NFB = Feet<T>::N;       /* feet: phase-3 implicit contact vectors [NFB][ND][6] at TAU */
-    static constexpr int U2A = NTL * ND + NS * CJN, U2B = 6 * NFB * ND;
+    static constexpr int FD = 6 * NFB * ND;      /* phase 3: [ND][6] I^c S_d (after Y, relative to TAU)     */
+    static constexpr int U2A = NTL * ND + NS * CJN, U2B = 6 * (NFB + 1) * ND;
     static constexpr int U1 = 24 * (NB + 1) + 6 * ND, U2 = U2A > U2B ? U2A : U2B;
     static constexpr int U3 = OBSMAX + 6 * (T::NOS + 1);
     static constexpr int USZ = U1 > U2 ? (U1 > U3 ? U1 : U3) : (U2 > U3 ? U2 : U3);
@@ -1358,8 +1359,24 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
         for (int li = 0; li < T::NL; ++li)
             if (SM.lim_dof[li] == lane) r += lds[LY::LIM + 4 * li + 2];
         lds[LY::RHS + lane] = r;
+        /* F_d = I^c S_d, the composite inertia of dof d's body times its
+         * column: entry (l, k) of M is S_other . F_deeper */
+        Real Fd[6];
+        {
+            const Real *ic = lds + LY::IC + 10 * SM.dof_cb[lane];
+            Real t[3];
+            symv(ic + 4, Sd, Fd);
+            cross3(ic + 1, Sd + 3, t);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) Fd[i] += t[i];
+            cross3(Sd, ic + 1, t);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) Fd[3 + i] = ic[0] * Sd[3 + i] + t[i];
+        }
+        wave_sync_lanes();   /* every dof lane has read the torque and contact slots */
+#pragma unroll
+        for (int i = 0; i < 6; ++i) lds[LY::TAU + LY::FD + 6 * lane + i] = Fd[i];
         if (implicit) {
-            wave_sync_lanes();   /* every dof lane has read the torque slots */
 #pragma unroll
             for (int b = 0; b < FT::N; ++b)
 #pragma unroll
@@ -1368,20 +1385,13 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     }
     wave_sync();
     for (int e = lane; e < NP; e += G) {
-        int l = SM.e_l[e], k = SM.e_k[e], c = SM.e_c[e];
-        const Real *Sl = lds + LY::S + 6 * l, *Sk = lds + LY::S + 6 * k;
+        const uint32_t ep = SM.e_pk[e];
+        const int l = ep & 0xff, k = (ep >> 8) & 0xff, dp = (ep >> 16) & 0xff, ot = ep >> 24;
+        const Real *Sl = lds + LY::S + 6 * l;
         Real v = 0;
-        if (c >= 0) {
-            const Real *ic = lds + LY::IC + 10 * c;
-            Real Lm[3], Pm[3], t[3];
-            symv(ic + 4, Sl, Lm);
-            cross3(ic + 1, Sl + 3, t);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) Lm[i] += t[i];
-            cross3(Sl, ic + 1, t);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) Pm[i] = ic[0] * Sl[3 + i] + t[i];
-            v = dot3(Sk, Lm) + dot3(Sk + 3, Pm);
+        if (dp != 0xff) {
+            const Real *So = lds + LY::S + 6 * ot, *Fp = lds + LY::TAU + LY::FD + 6 * dp;
+            v = dot3(So, Fp) + dot3(So + 3, Fp + 3);
         }
         if (implicit) {
             /* implicit contact: S_l . Y_{b,k} for each foot b both dofs move */
@@ -1607,7 +1617,9 @@ __global__ __launch_bounds__(BIOIM_WG) void id_kernel(IdArgs<T, Real> a) {
     wave_sync();
     if (need_m) {
         for (int e = lane; e < NP; e += G) {
-            const int l = SM.e_l[e], k = SM.e_k[e], c = SM.e_c[e];
+            const uint32_t ep = SM.e_pk[e];
+            const int l = ep & 0xff, k = (ep >> 8) & 0xff, dp = (ep >> 16) & 0xff;
+            const int c = dp != 0xff ? SM.dof_cb[dp] : -1;
             const Real *Sl = lds + LY::S + 6 * l, *Sk = lds + LY::S + 6 * k;
             Real val = 0;
             if (c >= 0) {
@@ -2398,8 +2410,9 @@ template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, 
     for (int l = 0, e = 0; l < p.ndof; ++l)
         for (int k = 0; k <= l; ++k, ++e) {
             int cl = m.dof_cb[l], ck = m.dof_cb[k];
-            m.e_l[e] = l; m.e_k[e] = k;
-            m.e_c[e] = ((T::anc[cl] >> ck) & 1u) ? cl : (((T::anc[ck] >> cl) & 1u) ? ck : -1);
+            const int c = ((T::anc[cl] >> ck) & 1u) ? cl : (((T::anc[ck] >> cl) & 1u) ? ck : -1);
+            const int dp = c < 0 ? 0xff : (c == cl ? l : k), ot = c < 0 ? 0 : (c == cl ? k : l);
+            m.e_pk[e] = (uint32_t)l | ((uint32_t)k << 8) | ((uint32_t)dp << 16) | ((uint32_t)ot << 24);
         }
 }
 
