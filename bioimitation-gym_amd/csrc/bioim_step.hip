@@ -50,12 +50,16 @@ DEV void sfor(F &&f) {
 template <typename Real> struct Eps;
 template <> struct Eps<float> {
     static constexpr float u_tol = 2e-7f;   /* Bezier parameter tolerance  */
+    static constexpr float u_stop = 2e-7f;  /* Newton step after which the root is converged */
     static constexpr float v_tol = 1e-7f;   /* normalized velocity         */
     static constexpr float l_tol = 1e-9f;   /* fiber length (m)            */
     static constexpr int it_max = 24;
 };
 template <> struct Eps<double> {
     static constexpr double u_tol = 1e-15;
+    /* a Newton step of at most 1e-11 leaves an error ~ |g''/2g'| 1e-22 in u
+     * (quadratic convergence; the smooth curves have |g''/g'| = O(10)) */
+    static constexpr double u_stop = 1e-11;
     static constexpr double v_tol = 1e-15;
     static constexpr double l_tol = 1e-15;
     static constexpr int it_max = 60;
@@ -320,7 +324,7 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
         Real du = fabs(un - u);
         u = un;
         /* converged, or stagnating at the rounding level of g */
-        if (it >= 1 && (du <= Eps<Real>::u_tol || (du <= Real(1e3) * Eps<Real>::u_tol && du >= Real(0.5) * dprev))) {
+        if (it >= 1 && (du <= Eps<Real>::u_stop || (du <= Real(1e3) * Eps<Real>::u_tol && du >= Real(0.5) * dprev))) {
 #ifdef BIOIM_STAMPS
             if (blockIdx.x == 0 && threadIdx.x < 14) atomicAdd(&g_stamps[12], (unsigned long long)(it + 1));
             if (blockIdx.x == 0 && threadIdx.x < 14) atomicAdd(&g_stamps[13], 1ull);
