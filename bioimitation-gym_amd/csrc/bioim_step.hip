@@ -1186,6 +1186,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
      * location functions (read by every muscle that has the point) and the
      * joints' spline axes (read by their body's lane) */
     fn_slots<T, Real>(SM, lds, lane);
+    STAMP(15);
 
     /* ---- phase 1: lane-parallel kinematics */
     if (lane < NB) kin_local<T, Real>(SM, lds, lane);

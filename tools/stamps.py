@@ -26,9 +26,10 @@ for k in range(steps):
     env.step(acts[5 + k])
 torch.cuda.synchronize()
 f(buf, 1)
-names = ['kin local (lane=body)', 'kin compose (levels)', 'columns + inertias', 'subtree sums', 'muscle path',
+names = ['kin local (after slots)', 'kin compose (levels)', 'columns + inertias', 'subtree sums', 'muscle path',
          'muscle eval / actuators', 'contacts', 'limits + sync', 'M entries + rhs', 'cholesky']
-tot = sum(buf[i] for i in range(len(names)))
+tot = sum(buf[i] for i in range(len(names))) + buf[15]
+print(f'  publish + function slots (phase 0/0b) {buf[15] / (steps * (env.nsub + 1)):9.0f} cyc  {100.0 * buf[15] / tot:5.1f} %')
 calls = steps * (env.nsub + 1)
 print(f'{env_id} fp{prec}: cycles per dynamics call {tot / calls:.0f} (workgroup 0, env 0)')
 for i, n in enumerate(names):
