@@ -348,6 +348,21 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
     }
 }
 
+/* muscle of lane slot s (slot = lane + j * G): when the muscles take two
+ * passes over the lanes, the second, partly idle pass holds the cheapest
+ * paths (T::mperm, tools/build_packs.py); a bijection of [0, NM), the
+ * identity elsewhere, so slot-range checks stay valid */
+template <class T> DEV int mslot(int s) {
+    int r = s;
+    if constexpr (T::NM > T::G) {
+        sfor<0, T::NM>([&](auto iI) {
+            constexpr int i = decltype(iI)::value;
+            r = s == i ? T::mperm[i] : r;
+        });
+    }
+    return r;
+}
+
 /* composite bodies carrying contact spheres (the feet), in first-appearance
  * order of T::sphere_cb */
 template <class T> struct Feet {
@@ -1249,7 +1264,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
         for (int d = 0; d < ND; ++d) tau[d] = 0;
         sfor<0, MPL>([&](auto jI) {
             constexpr int j = decltype(jI)::value;
-            const int m = lane + j * G;
+            const int m = mslot<T>(lane + j * G);
             if (m < T::NM) {
                 const SMuscle<Real> &mu = SM.mus[m];
                 Real L, dLs[T::MAXSPAN];
@@ -1282,7 +1297,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
         for (int d = 0; d < ND; ++d) tau[d] = 0;
         sfor<0, MPL>([&](auto jI) {
             constexpr int j = decltype(jI)::value;
-            const int m = lane + j * G;
+            const int m = mslot<T>(lane + j * G);
             if (m < T::NA) {
                 const int ad = SM.act_dof[m];
                 const Real f = control[j] * SM.ca_opt[m];
@@ -1769,7 +1784,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     Real act[MPL], lce[MPL], control[MPL], curr[MPL], last[MPL], hist[MPL][BIOIM_MAX_HORIZON];
 #pragma unroll
     for (int j = 0; j < MPL; ++j) {
-        const int m = lane + j * G;
+        const int m = mslot<T>(lane + j * G);
         act[j] = 0; lce[j] = 0; control[j] = 0; curr[j] = 0; last[j] = 0;
         if (NM > 0 && m < NM) { act[j] = st.act[(size_t)m * N + env]; lce[j] = st.lce[(size_t)m * N + env]; }
 #pragma unroll
@@ -1798,7 +1813,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         bool nan_here = false;
 #pragma unroll
         for (int j = 0; j < MPL; ++j) {
-            const int m = lane + j * G;
+            const int m = mslot<T>(lane + j * G);
             raw[j] = m < NA ? actions[(size_t)env * a.act_stride + m] : Real(0);
             nan_here = nan_here || (m < NA && isnan(raw[j]));
         }
@@ -1813,7 +1828,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             if (!anynan) {
 #pragma unroll
                 for (int j = 0; j < MPL; ++j) {
-                    const int m = lane + j * G;
+                    const int m = mslot<T>(lane + j * G);
                     Real xq = 0, xu = 0;
                     sfor<0, NA>([&](auto iI) {
                         constexpr int i = decltype(iI)::value;
@@ -1826,7 +1841,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         bool pnan_here = false;
 #pragma unroll
         for (int j = 0; j < MPL; ++j) {
-            const int m = lane + j * G;
+            const int m = mslot<T>(lane + j * G);
             if (!has_last) {
                 last[j] = av[j];
 #pragma unroll
@@ -1859,7 +1874,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         const bool pnan = group_any<G>(pnan_here);
 #pragma unroll
         for (int j = 0; j < MPL; ++j) {
-            const int m = lane + j * G, ms = m < NA ? m : 0;
+            const int m = mslot<T>(lane + j * G), ms = m < NA ? m : 0;
             const Real lo = NM > 0 ? Real(0) : SM.ca_min[ms];
             const Real hi = NM > 0 ? Real(1) : SM.ca_max[ms];
             const Real v = pnan ? Real(0) : control[j];
@@ -1916,7 +1931,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             if constexpr (NM > 0) {
 #pragma unroll
                 for (int j = 0; j < MPL; ++j) {
-                    const int m = lane + j * G;
+                    const int m = mslot<T>(lane + j * G);
                     if (m < NM) {
                         act[j] += dt * D.ms[j].dadt;
                         if (!D.ms[j].clamped) {
@@ -1986,7 +2001,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         if constexpr (NM > 0) {
 #pragma unroll
             for (int j = 0; j < MPL; ++j) {
-                const int m = lane + j * G;
+                const int m = mslot<T>(lane + j * G);
                 if (m < NM) {
                     ob[omus + 3 * m] = D.ms[j].act;
                     ob[omus + 3 * m + 1] = D.ms[j].lce;
@@ -2062,7 +2077,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                 Real an = 0, cot = 0;
 #pragma unroll
                 for (int j = 0; j < MPL; ++j) {
-                    const int m = lane + j * G;
+                    const int m = mslot<T>(lane + j * G);
                     if (m < NM) {
                         an += D.ms[j].act * D.ms[j].act;
                         const SMuscle<Real> &mu = SM.mus[m];
@@ -2155,7 +2170,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     }
 #pragma unroll
     for (int j = 0; j < MPL; ++j) {
-        const int m = lane + j * G;
+        const int m = mslot<T>(lane + j * G);
         if (NM > 0 && m < NM) { st.act[(size_t)m * N + env] = act[j]; st.lce[(size_t)m * N + env] = lce[j]; }
         if (m < NA) {
             st.last[(size_t)m * N + env] = last[j];

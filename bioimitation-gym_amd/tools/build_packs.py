@@ -104,7 +104,7 @@ def unique_curves(pk):
     return seen
 
 
-def emit_topology(struct, pk, lanes):
+def emit_topology(struct, pk, lanes):  # noqa: C901
     nb, nd, nc, nm = pk.ncbody, pk.ndof, pk.ncoord, pk.nmuscle
     parent = [pk.cbody[c].parent for c in range(nb)]
     anc = []
@@ -161,6 +161,18 @@ def emit_topology(struct, pk, lanes):
         maxspan = max(maxspan, bin(u & ~root).count('1'))
     s += f'    static constexpr int MAXPT = {maxpt}; /* path points per muscle (max) */\n'
     s += f'    static constexpr int MAXSPAN = {maxspan}; /* non-root dofs a muscle path moves (max) */\n'
+    # muscle slot -> muscle: when muscles take two passes over the lanes (NM > G), the second,
+    # partly idle pass gets the cheapest paths (fewest points, no moving/conditional points)
+    def cost(i):
+        m = pk.muscle[i]
+        t = [pk.pathpt[m.pt_off + j].type for j in range(m.npt)]
+        return m.npt + 3 * t.count(2) + t.count(1)
+    if nm > lanes:
+        order = sorted(range(nm), key=lambda i: (-cost(i), i))
+        mperm = sorted(order[:lanes]) + sorted(order[lanes:], key=lambda i: (cost(i), i))
+    else:
+        mperm = list(range(nm))
+    s += _carr('mperm', mperm or [0])
     nmf = sum(1 for j in range(pk.npathpt) if pk.pathpt[j].type == 2 for a in range(3) if pk.pathpt[j].fn[a] >= 0)
     s += f'    static constexpr int NMF = {nmf}; /* moving-point location functions (one lane each, per dynamics call) */\n'
     s += f'    static constexpr unsigned PT_COND = {cond}u, PT_MOVING = {move}u; /* point indices that can be conditional / moving */\n'
