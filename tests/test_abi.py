@@ -42,3 +42,48 @@ def test_create_without_gpu_fails_loudly():
     from bioimitation.vector_env import VectorEnv
     with pytest.raises(_lib.BioimError):
         VectorEnv('MuscleWalkingImitation2D-v0', 4)
+
+
+def _lib_or_skip():
+    from bioimitation import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip('libbioim.so not built')
+    return _lib, _lib.load()
+
+
+def test_entry_points_reject_bad_arguments_without_touching_a_gpu():
+    """Argument checks run before any device call: null handles and bad
+    sizes return BIOIM_E_ARG (-1) with a message (include/bioim.h error
+    convention), on a machine without a GPU too."""
+    _lib, L = _lib_or_skip()
+    from bioimitation.registry import load_pack
+    vp = C.c_void_p
+    h = vp()
+    pk = load_pack('MuscleWalkingImitation2D-v0')
+    assert L.bioim_create(None, 4, 0, 64, 0, C.byref(h)) == -1
+    assert b'bad arguments' in L.bioim_last_error()
+    assert L.bioim_create(C.byref(pk), 0, 0, 64, 0, C.byref(h)) == -1
+    assert L.bioim_create(C.byref(pk), 4, 0, 16, 0, C.byref(h)) == -1
+    assert b'precision' in L.bioim_last_error()
+    assert L.bioim_reset(None, None, None, 1, None) == -1
+    assert L.bioim_step(None, None, None, None, None, None) == -1
+    assert L.bioim_set_auto_reset(None, 1) == -1
+    assert L.bioim_set_env_offset(None, 0) == -1
+    assert L.bioim_set_io_strides(None, 1, 1, 1) == -1
+    assert L.bioim_step_group(None, 0, None, None, None, None, None) == -1
+    assert L.bioim_set_perturbation(None, 0, 0, None, None) == -1
+    assert L.bioim_id_eval(None, 0, 1, None, None, None, None) == -1
+    assert L.bioim_get_state(None, None) == -1 and L.bioim_set_state(None, None) == -1
+    assert L.bioim_query(None, None) == -1 and L.bioim_query_launch(None, None) == -1
+    assert L.bioim_sync(None) == -1 and L.bioim_destroy(None) == 0
+    assert L.bioim_modelpack_size() == C.sizeof(pk)
+
+
+def test_create_rejects_a_pack_with_a_bad_magic():
+    _lib, L = _lib_or_skip()
+    from bioimitation.registry import load_pack
+    pk = load_pack('TorqueWalkingImitation2D-v0')
+    pk.magic = 0
+    h = C.c_void_p()
+    assert L.bioim_create(C.byref(pk), 4, 0, 64, 0, C.byref(h)) == -3     # BIOIM_E_PACK
+    assert b'magic' in L.bioim_last_error()
