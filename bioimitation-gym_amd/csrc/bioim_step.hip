@@ -843,6 +843,83 @@ template <int N, typename Real> DEV bool cholesky_solve(Real *A, Real *b) {
     return ok;
 }
 
+/* Tree-sparse LTL factorization M = L^T L and solve (Featherstone, Rigid
+ * Body Dynamics Algorithms 6.3), unrolled at compile time over the
+ * topology's dof tree: entry (k, i) of M is structurally non-zero only when
+ * i is k or an ancestor dof of k, and factoring from the leaves up creates
+ * no fill-in, so only those entries are touched (2D: 53 of the dense 121
+ * multiply-adds, 3D: 257 of 457).  In place on the packed lower M; returns
+ * false if not SPD. */
+template <class T> struct DofTree {
+    /* parent dof: the previous dof of the same body, else the last dof of
+     * the nearest ancestor body that has one, else -1 */
+    static constexpr int par(int d) {
+        for (int e = d - 1; e >= 0; --e)
+            if (T::dof_cb[e] == T::dof_cb[d]) return e;
+        for (int b = T::parent[T::dof_cb[d]]; b >= 0; b = T::parent[b]) {
+            int last = -1;
+            for (int e = 0; e < T::ND; ++e)
+                if (T::dof_cb[e] == b) last = e;
+            if (last >= 0) return last;
+        }
+        return -1;
+    }
+    /* i is a proper ancestor dof of k */
+    static constexpr bool anc(int k, int i) {
+        for (int j = par(k); j >= 0; j = par(j))
+            if (j == i) return true;
+        return false;
+    }
+};
+
+template <class T, int N, typename Real> DEV bool ltl_solve(Real *A, Real *b) {
+    using DT = DofTree<T>;
+    bool ok = true;
+    Real inv[N];
+    /* factor: for k = N-1 .. 0 */
+    sfor<0, N>([&](auto kk) {
+        constexpr int k = N - 1 - decltype(kk)::value;
+        Real s = A[tri<0>(k, k)];
+        ok = ok && (s > 0);
+        const Real d = sqrt(s > 0 ? s : Real(1e-30));
+        const Real id = fast_rcp(d);
+        inv[k] = id;
+        A[tri<0>(k, k)] = d;
+        sfor<0, N>([&](auto iI) {
+            constexpr int i = decltype(iI)::value;
+            if constexpr (DT::anc(k, i)) A[tri<0>(k, i)] *= id;
+        });
+        sfor<0, N>([&](auto iI) {
+            constexpr int i = decltype(iI)::value;
+            if constexpr (DT::anc(k, i)) {
+                sfor<0, N>([&](auto jI) {
+                    constexpr int j = decltype(jI)::value;
+                    if constexpr (j == i || DT::anc(i, j)) A[tri<0>(i, j)] -= A[tri<0>(k, i)] * A[tri<0>(k, j)];
+                });
+            }
+        });
+    });
+    /* L^T y = b, leaves first */
+    sfor<0, N>([&](auto ii) {
+        constexpr int i = N - 1 - decltype(ii)::value;
+        b[i] *= inv[i];
+        sfor<0, N>([&](auto jI) {
+            constexpr int j = decltype(jI)::value;
+            if constexpr (DT::anc(i, j)) b[j] -= A[tri<0>(i, j)] * b[i];
+        });
+    });
+    /* L x = y, root first */
+    sfor<0, N>([&](auto iI) {
+        constexpr int i = decltype(iI)::value;
+        sfor<0, N>([&](auto jI) {
+            constexpr int j = decltype(jI)::value;
+            if constexpr (DT::anc(i, j)) b[i] -= A[tri<0>(i, j)] * b[j];
+        });
+        b[i] *= inv[i];
+    });
+    return ok;
+}
+
 /* ---------------------------------------------------- contact + limits */
 template <typename Real> DEV Real smooth_step(Real y0, Real y1, Real x0, Real x1, Real x) {
     if (x <= x0) return y0;
@@ -1441,7 +1518,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     for (int e = 0; e < NP; ++e) A[e] = lds[LY::MP + e];
 #pragma unroll
     for (int d = 0; d < ND; ++d) xs[d] = lds[LY::RHS + d];
-    D.ok = cholesky_solve<ND, Real>(A, xs);
+    D.ok = ltl_solve<T, ND, Real>(A, xs);
     Real x = 0;
 #pragma unroll
     for (int d = 0; d < ND; ++d) x = lane == d ? xs[d] : x;
@@ -1666,7 +1743,7 @@ __global__ __launch_bounds__(BIOIM_WG) void id_kernel(IdArgs<T, Real> a) {
         for (int e = 0; e < NP; ++e) A[e] = lds[LY::MP + e];
 #pragma unroll
         for (int d = 0; d < ND; ++d) xs[d] = lds[LY::RHS + d];
-        cholesky_solve<ND, Real>(A, xs);
+        ltl_solve<T, ND, Real>(A, xs);
 #pragma unroll
         for (int d = 0; d < ND; ++d) r = lane == d ? xs[d] : r;
     } else if (lane < ND) {
