@@ -241,6 +241,19 @@ DEV float fast_rcp(float x) {
     float r = __builtin_amdgcn_rcpf(x);
     return fmaf(r, fmaf(-x, r, 1.0f), r);
 }
+/* 1/sqrt(x) for x > 0: hardware rsq plus two Newton refinements; a length
+ * and its inverse then cost one rsq (len = x * rsqrt(x)) instead of an IEEE
+ * sqrt and a reciprocal */
+DEV double fast_rsqrt(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    const double hx = 0.5 * x;
+    y = fma(y, fma(-hx * y, y, 0.5), y);
+    return fma(y, fma(-hx * y, y, 0.5), y);
+}
+DEV float fast_rsqrt(float x) {
+    float y = __builtin_amdgcn_rsqf(x);
+    return fmaf(y, fmaf(-0.5f * x * y, y, 0.5f), y);
+}
 
 /* a quintic segment in the power basis c[0] + c[1] u + ... + c[5] u^5
  * (converted from the Bezier control points at create time, convert_curve):
@@ -881,8 +894,8 @@ template <class T, int N, typename Real> DEV bool ltl_solve(Real *A, Real *b) {
         constexpr int k = N - 1 - decltype(kk)::value;
         Real s = A[tri<0>(k, k)];
         ok = ok && (s > 0);
-        const Real d = sqrt(s > 0 ? s : Real(1e-30));
-        const Real id = fast_rcp(d);
+        const Real sp = s > 0 ? s : Real(1e-30);
+        const Real id = fast_rsqrt(sp), d = sp * id;
         inv[k] = id;
         A[tri<0>(k, k)] = d;
         sfor<0, N>([&](auto iI) {
@@ -974,11 +987,13 @@ DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, int s, Real h) {
     }
     Real F[3] = {0, fn, 0};
     Real vt0 = -vs[0], vt2 = -vs[2];
-    Real vslip = sqrt(vt0 * vt0 + vt2 * vt2);
+    const Real vs2 = vt0 * vt0 + vt2 * vt2;
+    const Real ivs_ = vs2 > 0 ? fast_rsqrt(vs2) : Real(0);
+    Real vslip = vs2 * ivs_;
     Real vtr = SM.cf_vt[fo], ms = SM.cf_ms[fo], md = SM.cf_md[fo], mv = SM.cf_mv[fo];
     const Real ivtr = fast_rcp(vtr);
     Real r_ = vslip * ivtr, den = Real(1) + r_ * r_;
-    const Real iden = fast_rcp(den), ivs = vslip > 0 ? fast_rcp(vslip) : Real(0);
+    const Real iden = fast_rcp(den), ivs = ivs_;
     if (vslip != 0) {
         Real ff = fn * (fmin(r_, Real(1)) * (md + Real(2) * (ms - md) * iden) + mv * vslip);
         F[0] += ff * vt0 * ivs;
@@ -1038,8 +1053,8 @@ DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_
     Real a = a_state < mu.amin ? mu.amin : (a_state > Real(1) ? Real(1) : a_state);
     Real lce = l_state < mu.lmin ? mu.lmin : l_state;
     Real w = mu.width;
-    Real sq = sqrt(lce * lce - w * w);
-    const Real isq = fast_rcp(sq);
+    const Real sq2 = lce * lce - w * w;
+    const Real isq = fast_rsqrt(sq2), sq = sq2 * isq;
     const Real icos = lce * isq;          /* 1 / cos(pennation) */
     Real lt = L - sq;
     Real fse, dfse, fal, dfal, fpe, dfpe;
@@ -1192,9 +1207,9 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
                 Real e[3] = {0, 0, 0};
                 if (have) {
                     Real sgm[3] = {P[0] - Pp[0], P[1] - Pp[1], P[2] - Pp[2]};
-                    Real len = sqrt(dot3(sgm, sgm));
+                    const Real l2 = dot3(sgm, sgm);
+                    const Real inv = fast_rsqrt(l2), len = l2 * inv;
                     L += len;
-                    Real inv = fast_rcp(len);
 #pragma unroll
                     for (int a = 0; a < 3; ++a) e[a] = sgm[a] * inv;
                     Real g[3] = {ep[0] - e[0], ep[1] - e[1], ep[2] - e[2]};
