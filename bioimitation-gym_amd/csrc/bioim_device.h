@@ -135,6 +135,7 @@ struct SModel {
     Real cf_kk[D::NFD], cf_c[D::NFD], cf_ms[D::NFD], cf_md[D::NFD], cf_mv[D::NFD], cf_vt[D::NFD];
     /* coordinate limit forces (lane = limit) */
     Real lim_qup[D::NLD], lim_qlow[D::NLD], lim_kup[D::NLD], lim_klow[D::NLD], lim_damp[D::NLD], lim_trans[D::NLD];
+    Real lim_itrans[D::NLD];   /* 1 / transition width */
     /* coordinate actuators / PD gains (lane = actuator) */
     Real ca_opt[D::NAD], ca_min[D::NAD], ca_max[D::NAD], kp[D::NAD], kv[D::NAD];
     /* index tables */

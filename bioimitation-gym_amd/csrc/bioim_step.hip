@@ -934,16 +934,16 @@ template <class T, int N, typename Real> DEV bool ltl_solve(Real *A, Real *b) {
 }
 
 /* ---------------------------------------------------- contact + limits */
-template <typename Real> DEV Real smooth_step(Real y0, Real y1, Real x0, Real x1, Real x) {
+template <typename Real> DEV Real smooth_step(Real y0, Real y1, Real x0, Real x1, Real iw, Real x) {
     if (x <= x0) return y0;
     if (x >= x1) return y1;
-    Real t = (x - x0) / (x1 - x0);
+    Real t = (x - x0) * iw;   /* iw = 1 / (x1 - x0) */
     return y0 + (y1 - y0) * t * t * t * (Real(10) + t * (Real(6) * t - Real(15)));
 }
-template <typename Real> DEV Real smooth_step_d(Real y0, Real y1, Real x0, Real x1, Real x) {
+template <typename Real> DEV Real smooth_step_d(Real y0, Real y1, Real x0, Real x1, Real iw, Real x) {
     if (x <= x0 || x >= x1) return 0;
-    Real w = x1 - x0, t = (x - x0) / w;
-    return (y1 - y0) * Real(30) * t * t * (Real(1) - t) * (Real(1) - t) / w;
+    Real t = (x - x0) * iw;
+    return (y1 - y0) * Real(30) * t * t * (Real(1) - t) * (Real(1) - t) * iw;
 }
 
 /* Hunt-Crossley sphere s (this lane) vs the ground plane.  Publishes the
@@ -975,7 +975,8 @@ DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, int s, Real h) {
         for (int i = 0; i < 3; ++i) vs[i] = kb[15 + i] + t[i];
         vn = -vs[1];
         Real kk = SM.cf_kk[fo];
-        fH = Real(4.0 / 3.0) * kk * depth * sqrt(rad * kk * depth);
+        const Real rkd = rad * kk * depth;
+        fH = Real(4.0 / 3.0) * kk * depth * (rkd * fast_rsqrt(rkd));
         fn = fH * (Real(1) + Real(1.5) * SM.cf_c[fo] * vn);
     }
     bool active = fn > 0;
@@ -1408,14 +1409,14 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     if (lane < T::NL) {
         int cc = SM.lim_coord[lane];
         Real qv = lds[LY::QF + cc], qd = lds[LY::UF + cc];
-        Real qup = SM.lim_qup[lane], qlo = SM.lim_qlow[lane], tr = SM.lim_trans[lane];
-        Real up = smooth_step(Real(0), Real(1), qup, qup + tr, qv);
-        Real lo = smooth_step(Real(1), Real(0), qlo - tr, qlo, qv);
+        Real qup = SM.lim_qup[lane], qlo = SM.lim_qlow[lane], tr = SM.lim_trans[lane], itr = SM.lim_itrans[lane];
+        Real up = smooth_step(Real(0), Real(1), qup, qup + tr, itr, qv);
+        Real lo = smooth_step(Real(1), Real(0), qlo - tr, qlo, itr, qv);
         Real f = -SM.lim_kup[lane] * up * (qv - qup) + SM.lim_klow[lane] * lo * (qlo - qv) - SM.lim_damp[lane] * (up + lo) * qd;
         Real diag = 0, tadd = f;
         if (h > 0) {
-            Real dup = smooth_step_d(Real(0), Real(1), qup, qup + tr, qv);
-            Real dlo = smooth_step_d(Real(1), Real(0), qlo - tr, qlo, qv);
+            Real dup = smooth_step_d(Real(0), Real(1), qup, qup + tr, itr, qv);
+            Real dlo = smooth_step_d(Real(1), Real(0), qlo - tr, qlo, itr, qv);
             Real kq = SM.lim_kup[lane] * (up + dup * (qv - qup)) + SM.lim_klow[lane] * (lo - dlo * (qlo - qv));
             Real cq = SM.lim_damp[lane] * (up + lo);
             diag = h * cq + h * h * kq;
@@ -1720,8 +1721,9 @@ __global__ __launch_bounds__(BIOIM_WG) void id_kernel(IdArgs<T, Real> a) {
             const int cc = SM.lim_coord[lane];
             const Real qv = lds[LY::QF + cc], qdv = lds[LY::UF + cc];
             const Real qup = SM.lim_qup[lane], qlo = SM.lim_qlow[lane], tr = SM.lim_trans[lane];
-            const Real up = smooth_step(Real(0), Real(1), qup, qup + tr, qv);
-            const Real lo = smooth_step(Real(1), Real(0), qlo - tr, qlo, qv);
+            const Real itr = SM.lim_itrans[lane];
+            const Real up = smooth_step(Real(0), Real(1), qup, qup + tr, itr, qv);
+            const Real lo = smooth_step(Real(1), Real(0), qlo - tr, qlo, itr, qv);
             lds[LY::LIM + 4 * lane] = -SM.lim_kup[lane] * up * (qv - qup) + SM.lim_klow[lane] * lo * (qlo - qv) -
                                       SM.lim_damp[lane] * (up + lo) * qdv;
         }
@@ -2499,6 +2501,7 @@ template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, 
         const bioim_limit_t &s = p.limit[l];
         m.lim_qup[l] = (Real)s.qup; m.lim_qlow[l] = (Real)s.qlow; m.lim_kup[l] = (Real)s.kup;
         m.lim_klow[l] = (Real)s.klow; m.lim_damp[l] = (Real)s.damping; m.lim_trans[l] = (Real)s.trans;
+        m.lim_itrans[l] = (Real)(1.0 / s.trans);
         m.lim_coord[l] = s.coord; m.lim_dof[l] = s.dof;
     }
     for (int a = 0; a < p.ncoordact; ++a) {
