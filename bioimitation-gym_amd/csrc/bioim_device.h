@@ -22,6 +22,10 @@ struct DCurve {
     Real cx[BIOIM_MAX_CURVESEG][6];
     Real cy[BIOIM_MAX_CURVESEG][6];
     Real xa[BIOIM_MAX_CURVESEG], xb[BIOIM_MAX_CURVESEG], ya[BIOIM_MAX_CURVESEG], yb[BIOIM_MAX_CURVESEG];
+    /* segment search keys: xsep[s] = end x of segment s for s < nseg - 1,
+     * +inf after (so the search needs no segment count); xa of unused
+     * segments is +inf too (never bracketed by the fiber-velocity search) */
+    Real xsep[BIOIM_MAX_CURVESEG];
     Real ut[BIOIM_MAX_CURVESEG][BIOIM_UTAB + 1]; /* u at uniform x nodes of each segment */
     Real inv_h[BIOIM_MAX_CURVESEG];               /* BIOIM_UTAB / (x_end - x_start)       */
     Real x0, y0, dydx0, x1, y1, dydx1;

@@ -275,7 +275,7 @@ DEV void curve_eval(const DCurve<Real> &C, Real x, Real &y, Real &dydx) {
     Real xc = x < C.x0 ? C.x0 : (x > C.x1 ? C.x1 : x);
     int k = 0;
 #pragma unroll
-    for (int s = 0; s < BIOIM_MAX_CURVESEG - 1; ++s) k += (s < C.nseg - 1 && xc > C.xb[s]) ? 1 : 0;
+    for (int s = 0; s < BIOIM_MAX_CURVESEG - 1; ++s) k += xc > C.xsep[s] ? 1 : 0;
     Real px[6], py[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) { px[i] = C.cx[k][i]; py[i] = C.cy[k][i]; }
@@ -303,7 +303,7 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
     Real g1 = afal * C.y1 + beta * C.x1 - rhs;
     int k = 0;
 #pragma unroll
-    for (int s = 1; s < BIOIM_MAX_CURVESEG; ++s) k += (s < C.nseg && afal * C.ya[s] + beta * C.xa[s] - rhs <= 0) ? 1 : 0;
+    for (int s = 1; s < BIOIM_MAX_CURVESEG; ++s) k += afal * C.ya[s] + beta * C.xa[s] - rhs <= 0 ? 1 : 0;
     Real px[6], py[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) { px[i] = C.cx[k][i]; py[i] = C.cy[k][i]; }
@@ -2338,8 +2338,9 @@ template <typename Real> void convert_curve(const bioim_curve_t &s, DCurve<Real>
         bernstein_to_power(s.x[i], cx);
         bernstein_to_power(s.y[i], cy);
         for (int j = 0; j < 6; ++j) { d.cx[i][j] = (Real)cx[j]; d.cy[i][j] = (Real)cy[j]; }
-        d.xa[i] = (Real)s.x[i][0]; d.xb[i] = (Real)s.x[i][5];
-        d.ya[i] = (Real)s.y[i][0]; d.yb[i] = (Real)s.y[i][5];
+        d.xa[i] = i < s.nseg ? (Real)s.x[i][0] : (Real)INFINITY; d.xb[i] = (Real)s.x[i][5];
+        d.ya[i] = i < s.nseg ? (Real)s.y[i][0] : Real(0); d.yb[i] = (Real)s.y[i][5];
+        d.xsep[i] = i < s.nseg - 1 ? (Real)s.x[i][5] : (Real)INFINITY;
     }
     for (int k = 0; k < BIOIM_MAX_CURVESEG; ++k) {
         if (k >= s.nseg) { d.inv_h[k] = 0; for (int i = 0; i <= BIOIM_UTAB; ++i) d.ut[k][i] = 0; continue; }
