@@ -816,46 +816,6 @@ template <typename Real> DEV void symv(const Real *J, const Real *v, Real *o) {
     o[0] = x; o[1] = y; o[2] = z;
 }
 
-/* in-place packed-lower Cholesky solve; returns false if not SPD.  One
- * reciprocal per column, reused by both substitutions (divisions sit on the
- * solve's critical path) */
-template <int N, typename Real> DEV bool cholesky_solve(Real *A, Real *b) {
-    bool ok = true;
-    Real inv[N];
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        Real s = A[tri<0>(j, j)];
-#pragma unroll
-        for (int k = 0; k < j; ++k) s -= A[tri<0>(j, k)] * A[tri<0>(j, k)];
-        ok = ok && (s > 0);
-        Real d = sqrt(s > 0 ? s : Real(1e-30));
-        inv[j] = Real(1) / d;
-        A[tri<0>(j, j)] = d;
-#pragma unroll
-        for (int i = j + 1; i < N; ++i) {
-            Real t = A[tri<0>(i, j)];
-#pragma unroll
-            for (int k = 0; k < j; ++k) t -= A[tri<0>(i, k)] * A[tri<0>(j, k)];
-            A[tri<0>(i, j)] = t * inv[j];
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        Real t = b[i];
-#pragma unroll
-        for (int k = 0; k < i; ++k) t -= A[tri<0>(i, k)] * b[k];
-        b[i] = t * inv[i];
-    }
-#pragma unroll
-    for (int i = N - 1; i >= 0; --i) {
-        Real t = b[i];
-#pragma unroll
-        for (int k = i + 1; k < N; ++k) t -= A[tri<0>(k, i)] * b[k];
-        b[i] = t * inv[i];
-    }
-    return ok;
-}
-
 /* Tree-sparse LTL factorization M = L^T L and solve (Featherstone, Rigid
  * Body Dynamics Algorithms 6.3), unrolled at compile time over the
  * topology's dof tree: entry (k, i) of M is structurally non-zero only when
@@ -1525,10 +1485,11 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     wave_sync();
     STAMP(8);
 
-    /* ---- phase 4: Cholesky solve, redundant in every lane's registers (the
-     * shortest dependency chain for these 9x9 / 14x14 systems; a lane-
-     * distributed factorization with one LDS round trip per column measured
-     * 7 % slower per step); lane d keeps q''_d and publishes it for the report */
+    /* ---- phase 4: tree-sparse LTL solve (ltl_solve), redundant in every
+     * lane's registers (the shortest dependency chain for these 9x9 / 14x14
+     * systems; a lane-distributed dense factorization with one LDS round trip
+     * per column measured 7 % slower per step); lane d keeps q''_d and
+     * publishes it for the report */
     Real A[NP], xs[ND];
 #pragma unroll
     for (int e = 0; e < NP; ++e) A[e] = lds[LY::MP + e];
