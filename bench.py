@@ -130,6 +130,13 @@ def main():
         t_max = float(tt[0])
     steps_total = world * n * a.steps
     value = steps_total / t_max
+    # done rate: an untimed pass over the same actions after the
+    # timed region, counting terminations on the device
+    dones = torch.zeros((), dtype=torch.float64, device=dev)
+    for k in range(a.warmup, total):
+        done = env.step(acts[k])[2]
+        dones += done.to(torch.float64).sum()
+    done_rate = float(dones) / (n * a.steps)
     if rank == 0:
         real_bytes = 8 if a.precision == 64 else 4
         if a.mixed:   # env-weighted mean over the segments
@@ -150,7 +157,7 @@ def main():
             if a.env_id == 'MuscleWalkingImitation2D-v0' and n == 4096 else f'env steps/sec, {a.env_id} @ {n} envs/GPU',
             'value': value, 'unit': 'env-steps/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
             'ms_per_step': t_max / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': f'f{a.precision}',
+            'vs_baseline': None, 'dtype': f'f{a.precision}', 'done_rate': done_rate,
             'data': 'synthetic: PCG64 U[0,1] muscle excitations; reference motion synthesized from the shipped 3D IK',
             'config': {'workload': f'{a.env_id} batched env.step, {n} envs/GPU, nsub={env.nsub}, auto-reset',
                        'envs_per_gpu': n, 'lanes_per_env': env.lanes_per_env, 'parallelism': f'env-shard x{world}',

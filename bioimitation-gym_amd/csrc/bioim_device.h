@@ -29,6 +29,7 @@ struct DCurve {
     Real ut[BIOIM_MAX_CURVESEG][BIOIM_UTAB + 1]; /* u at uniform x nodes of each segment */
     Real inv_h[BIOIM_MAX_CURVESEG];               /* BIOIM_UTAB / (x_end - x_start)       */
     Real x0, y0, dydx0, x1, y1, dydx1;
+    Real y_at0; /* y(0), host-evaluated: the fiber-velocity curve at rest (clamped fiber) */
     int32_t nseg, pad;
 };
 

@@ -1029,9 +1029,7 @@ DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_
     bool clamped = (l_state <= mu.lmin && vN <= 0) || l_state < mu.lmin;
     if (clamped) {
         vN = 0;
-        Real y, dy;
-        curve_eval(Cfv, Real(0), y, dy);
-        fvv = y;
+        fvv = Cfv.y_at0;
     }
     s.act = a;
     s.lce = lce;
@@ -2279,6 +2277,16 @@ double host_invert(const double *px, double x) {
     return 0.5 * (lo + hi);
 }
 
+/* y(x) of a pack curve, to machine precision (the device's curve_eval
+ * semantics: linear extrapolation outside [x0, x1]) */
+double host_curve_y(const bioim_curve_t &s, double x) {
+    if (x < s.x0) return s.y0 + s.dydx0 * (x - s.x0);
+    if (x > s.x1) return s.y1 + s.dydx1 * (x - s.x1);
+    int k = 0;
+    while (k < s.nseg - 1 && x > s.x[k][5]) ++k;
+    return host_bez5(s.y[k], host_invert(s.x[k], x));
+}
+
 /* Bernstein control points of a quintic -> power-basis coefficients:
  * c_j = C(5, j) sum_{k <= j} C(j, k) (-1)^(j-k) p_k */
 void bernstein_to_power(const double *p, double *c) {
@@ -2311,6 +2319,7 @@ template <typename Real> void convert_curve(const bioim_curve_t &s, DCurve<Real>
     }
     d.x0 = (Real)s.x0; d.y0 = (Real)s.y0; d.dydx0 = (Real)s.dydx0;
     d.x1 = (Real)s.x1; d.y1 = (Real)s.y1; d.dydx1 = (Real)s.dydx1;
+    d.y_at0 = s.nseg > 0 ? (Real)host_curve_y(s, 0.0) : Real(0);
     d.nseg = s.nseg;
 }
 
