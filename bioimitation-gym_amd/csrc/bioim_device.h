@@ -161,6 +161,10 @@ struct SModel {
     /* root-to-body joint chain, front-padded with the identity joint slot NB */
     int32_t chain[T::NB][TopoInfo<T>::depth()];
     int32_t sph_cb[D::NSD], sph_force[D::NSD], lim_coord[D::NLD], lim_dof[D::NLD], act_dof[D::NAD];
+    /* muscle torque gather (lane = dof): the TAU slots (muscle slot s, span
+     * entry k -> s * MAXSPAN + k) holding -F_t dL/dq_d, padded with the zero
+     * slot */
+    uint8_t tau_src[D::NDD][T::MAXARM];
 };
 
 /* bytes of the LDS image (16-byte granules for the cooperative copy) */

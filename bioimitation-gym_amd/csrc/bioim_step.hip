@@ -442,13 +442,17 @@ template <class T, typename Real> struct Lay {
     static constexpr int U = ((MF + 3 * (NSLOT > 0 ? NSLOT : 1) + 1) / 2) * 2;
     static constexpr int LOC = U;                /* phase 1: [NB+1][24] joint-local data (NB: identity) */
     static constexpr int SL = LOC + 24 * (NB + 1); /* phase 1: [ND][6] joint-local Plucker columns  */
-    static constexpr int TAU = U;                /* phases 2-3: [NTL][ND] per-lane muscle/actuator torques */
-    static constexpr int CJ = TAU + NTL * ND;    /* phases 2-3: [NS][CJN] contact slots             */
+    /* phases 2-3: muscles: [MPL * G][MAXSPAN] -F_t dL/dq over each muscle
+     * slot's span, then one zero slot (TZ); actuators: [NTL][ND] per-lane torques */
+    static constexpr int TZ = MPL * T::G * T::MAXSPAN;
+    static constexpr int TAUN = T::NM > 0 ? (TZ + 1 > NTL * ND ? TZ + 1 : NTL * ND) : NTL * ND;
+    static constexpr int TAU = U;
+    static constexpr int CJ = TAU + TAUN;        /* phases 2-3: [NS][CJN] contact slots             */
     static constexpr int OBS = U;                /* report: observation staging                     */
     static constexpr int REP = OBS + OBSMAX;     /* report: [NOS+1][6] body pos/vel (NOS: COM)      */
     static constexpr int NFB = Feet<T>::N;       /* feet: phase-3 implicit contact vectors [NFB][ND][6] at TAU */
     static constexpr int FD = 6 * NFB * ND;      /* phase 3: [ND][6] I^c S_d (after Y, relative to TAU)     */
-    static constexpr int U2A = NTL * ND + NS * CJN, U2B = 6 * (NFB + 1) * ND;
+    static constexpr int U2A = TAUN + NS * CJN, U2B = 6 * (NFB + 1) * ND;
     static constexpr int U1 = 24 * (NB + 1) + 6 * ND, U2 = U2A > U2B ? U2A : U2B;
     static constexpr int U3 = OBSMAX + 6 * (T::NOS + 1);
     static constexpr int USZ = U1 > U2 ? (U1 > U3 ? U1 : U3) : (U2 > U3 ? U2 : U3);
@@ -1305,14 +1309,13 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     }
     STAMP(3);
     if constexpr (T::NM > 0) {
-        /* this lane's muscles' -F_t dL/dq over their spans, accumulated in
-         * registers (compile-time dof indices) and stored as one torque
-         * slot.  (An LDS read-modify-write of the slot at the span's runtime
-         * dof indices, combined with the early deque store, produced wrong
-         * fp32 3D results on the GPU — DESIGN.md 5.1.) */
-        Real tau[ND];
-#pragma unroll
-        for (int d = 0; d < ND; ++d) tau[d] = 0;
+        /* this lane's muscles' -F_t dL/dq over their spans, stored per muscle
+         * slot and span entry (plain stores); the dof lanes gather them in
+         * phase 3 through SM.tau_src.  (An LDS read-modify-write of per-lane
+         * torque slots at the span's runtime dof indices, combined with the
+         * early deque store, produced wrong fp32 3D results on the GPU —
+         * DESIGN.md 5.1.) */
+        if (lane == 0) lds[LY::TAU + LY::TZ] = Real(0);
         sfor<0, MPL>([&](auto jI) {
             constexpr int j = decltype(jI)::value;
             const int m = mslot<T>(lane + j * G);
@@ -1330,18 +1333,11 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
                 D.lce[j] = l_;
                 muscle_eval<T, Real>(SM, mu, a_, l_, control[j], L, D.ms[j].vN, D.ms[j]);
                 const Real nFt = -D.ms[j].Ft;
+                Real *ts = lds + LY::TAU + (lane + j * G) * T::MAXSPAN;
 #pragma unroll
-                for (int k = 0; k < T::MAXSPAN; ++k) {
-                    const int dk = k < mu.nspan ? mu.span[k] : -1;
-#pragma unroll
-                    for (int d = 0; d < ND; ++d) tau[d] += dk == d ? nFt * dLs[k] : Real(0);
-                }
+                for (int k = 0; k < T::MAXSPAN; ++k) ts[k] = nFt * dLs[k];
             }
         });
-        if (lane < LY::NTL) {
-#pragma unroll
-            for (int d = 0; d < ND; ++d) lds[LY::TAU + ND * lane + d] = tau[d];
-        }
     } else {
         Real tau[ND];
 #pragma unroll
@@ -1399,8 +1395,13 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     if (lane < ND) {
         const Real *Sd = lds + LY::S + 6 * lane, *wb = lds + LY::WB + 6 * SM.dof_cb[lane];
         Real r = -(dot3(Sd, wb) + dot3(Sd + 3, wb + 3));
+        if constexpr (T::NM > 0) {
 #pragma unroll
-        for (int m = 0; m < LY::NTL; ++m) r += lds[LY::TAU + ND * m + lane];
+            for (int i = 0; i < T::MAXARM; ++i) r += lds[LY::TAU + SM.tau_src[lane][i]];
+        } else {
+#pragma unroll
+            for (int m = 0; m < LY::NTL; ++m) r += lds[LY::TAU + ND * m + lane];
+        }
         Real Y[FT::N > 0 ? FT::N : 1][6];
 #pragma unroll
         for (int b = 0; b < FT::N; ++b)
@@ -1455,7 +1456,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
         }
     }
     wave_sync();
-    for (int e = lane; e < NP; e += G) {
+    auto m_entry = [&](int e) {
         const uint32_t ep = SM.e_pk[e];
         const int l = ep & 0xff, k = (ep >> 8) & 0xff, dp = (ep >> 16) & 0xff, ot = ep >> 24;
         const Real *Sl = lds + LY::S + 6 * l;
@@ -1479,7 +1480,12 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
                     if (SM.lim_dof[li] == l) v += lds[LY::LIM + 4 * li + 1];
         }
         lds[LY::MP + e] = v;
-    }
+    };
+    /* all passes over the entries unrolled: their LDS loads can be issued
+     * ahead of the previous pass's FMAs */
+#pragma unroll
+    for (int pass = 0; pass < (NP + G - 1) / G; ++pass)
+        if ((pass + 1) * G <= NP || lane + pass * G < NP) m_entry(lane + pass * G);
     wave_sync();
     STAMP(8);
 
@@ -2395,6 +2401,22 @@ template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, 
             if ((u >> dd) & 1u) d.span[d.nspan++] = dd;
         for (int k = d.nspan; k < BIOIM_MAX_SPAN; ++k) d.span[k] = d.nspan ? d.span[0] : 0;
     }
+    {   /* muscle torque gather lists (Lay::TZ: the zero slot) */
+        using LY = Lay<T, Real>;
+        static_assert(LY::TZ < 256, "TAU slot indices are bytes");
+        for (int d = 0; d < SDim<T>::NDD; ++d)
+            for (int i = 0; i < T::MAXARM; ++i) m.tau_src[d][i] = (uint8_t)LY::TZ;
+        int cnt[SDim<T>::NDD] = {};
+        for (int sl = 0; sl < LY::MPL * T::G; ++sl) {
+            const int mi = (T::NM > T::G && sl < T::NM) ? T::mperm[sl] : sl;
+            if (mi >= p.nmuscle) continue;
+            for (int k = 0; k < m.mus[mi].nspan; ++k) {
+                const int d = m.mus[mi].span[k];
+                if (cnt[d] < T::MAXARM) m.tau_src[d][cnt[d]] = (uint8_t)(sl * T::MAXSPAN + k);
+                ++cnt[d];
+            }
+        }
+    }
     std::vector<uint32_t> dofmask(T::NB, 0);
     for (int c = 0; c < T::NB; ++c) dofmask[c] = T::dofmask[c];
     int nmf = 0;
@@ -2517,11 +2539,15 @@ template <class T> bool topology_matches(const bioim_modelpack_t &p) {
         if (nmf != T::NMF) return false;
         uint32_t root = ~0u;
         for (int c = 0; c < T::NB; ++c) root &= T::dofmask[c];
+        int arms[32] = {};
         for (int i = 0; i < p.nmuscle; ++i) {
             uint32_t u = 0;
             for (int j = 0; j < p.muscle[i].npt; ++j) u |= T::dofmask[p.pathpt[p.muscle[i].pt_off + j].cbody];
             if (__builtin_popcount(u & ~root) > T::MAXSPAN || T::MAXSPAN > BIOIM_MAX_SPAN) return false;
+            for (int d = 0; d < T::ND; ++d) arms[d] += ((u & ~root) >> d) & 1u;
         }
+        for (int d = 0; d < T::ND; ++d)
+            if (arms[d] > T::MAXARM) return false;
     }
     for (int f = 0; f < p.nfn; ++f)
         if (p.fn[f].nknots > T::NKMAX) return false;

@@ -152,15 +152,18 @@ def emit_topology(struct, pk, lanes):  # noqa: C901
     root = (1 << nd) - 1
     for c in range(nb):
         root &= dofmask[c]
-    maxspan = 1
+    maxspan, arms = 1, [0] * max(nd, 1)
     for i in range(pk.nmuscle):
         m = pk.muscle[i]
         u = 0
         for j in range(m.npt):
             u |= dofmask[pk.pathpt[m.pt_off + j].cbody]
         maxspan = max(maxspan, bin(u & ~root).count('1'))
+        for d in range(nd):
+            arms[d] += (u & ~root) >> d & 1
     s += f'    static constexpr int MAXPT = {maxpt}; /* path points per muscle (max) */\n'
     s += f'    static constexpr int MAXSPAN = {maxspan}; /* non-root dofs a muscle path moves (max) */\n'
+    s += f'    static constexpr int MAXARM = {max(arms + [1])}; /* muscles spanning one dof (max) */\n'
     # muscle slot -> muscle: when muscles take two passes over the lanes (NM > G), the second,
     # partly idle pass gets the cheapest paths (fewest points, no moving/conditional points)
     def cost(i):

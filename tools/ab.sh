@@ -1,25 +1,29 @@
 #!/bin/bash
-# Same-box A/B of two builds of libbioim.so (GPU box): alternates the
-# candidate (the in-tree build) and a baseline library (BIOIM_LIB=...) over
-# R rounds of bench.py, per env ID, and prints ms_per_step of each.
-#   bash tools/ab.sh <baseline.so> <out-dir> [rounds] [env ids...]
+# Same-box A/B of builds of libbioim.so (GPU box).  Alternates the libraries
+# over R rounds of bench.py per env ID and prints each one's kernel ms per
+# step (HIP events on the launch stream); "tree" is the in-tree build.
+#   bash tools/ab.sh <out-dir> <rounds> <id,id,...> <lib|tree> [<lib|tree> ...]
 set -e
-base=$1; out=$2; rounds=${3:-3}; shift 3 || true
-ids=${@:-MuscleWalkingImitation2D-v0 MuscleRunningImitation3D-v0}
+out=$1; rounds=$2; ids=$3; shift 3
 mkdir -p "$out"
-for id in $ids; do
+for id in ${ids//,/ }; do
   for r in $(seq 1 "$rounds"); do
-    timeout -k 10 120 python bench.py --no-cpu-baseline --env-id "$id" > "$out/new_${id}_$r.json"
-    BIOIM_LIB="$base" timeout -k 10 120 python bench.py --no-cpu-baseline --env-id "$id" > "$out/old_${id}_$r.json"
+    for lib in "$@"; do
+      tag=$(basename "$lib" .so)
+      if [ "$lib" = tree ]; then
+        timeout -k 10 120 python bench.py --no-cpu-baseline --env-id "$id" > "$out/${tag}__${id}__$r.json"
+      else
+        BIOIM_LIB="$lib" timeout -k 10 120 python bench.py --no-cpu-baseline --env-id "$id" > "$out/${tag}__${id}__$r.json"
+      fi
+    done
   done
 done
 python3 - "$out" <<'PY'
 import glob, json, os, sys, collections
 d = collections.defaultdict(list)
 for f in sorted(glob.glob(os.path.join(sys.argv[1], '*.json'))):
-    tag, rest = os.path.basename(f).split('_', 1)
-    env = rest.rsplit('_', 1)[0]
+    tag, env, _ = os.path.basename(f).split('__')
     d[(env, tag)].append(json.load(open(f))['roofline']['kernel_ms'])
 for (env, tag), v in sorted(d.items()):
-    print(f'{env:34s} {tag}: kernel ms ' + ' '.join(f'{x:.4f}' for x in v) + f'  min {min(v):.4f}')
+    print(f'{env:30s} {tag:22s} kernel ms ' + ' '.join(f'{x:.4f}' for x in v) + f'  min {min(v):.4f}')
 PY
