@@ -442,10 +442,11 @@ template <class T, typename Real> struct Lay {
     static constexpr int U = ((MF + 3 * (NSLOT > 0 ? NSLOT : 1) + 1) / 2) * 2;
     static constexpr int LOC = U;                /* phase 1: [NB+1][24] joint-local data (NB: identity) */
     static constexpr int SL = LOC + 24 * (NB + 1); /* phase 1: [ND][6] joint-local Plucker columns  */
-    /* phases 2-3: muscles: [MPL * G][MAXSPAN] -F_t dL/dq over each muscle
-     * slot's span, then one zero slot (TZ); actuators: [NTL][ND] per-lane torques */
+    /* phases 2-3: [MPL * G][MAXSPAN] per muscle slot, -F_t dL/dq over its
+     * span (actuator slot: its torque), then one zero slot (TZ); at least
+     * NTL * ND reals (the region is shared with the phase-3 vectors) */
     static constexpr int TZ = MPL * T::G * T::MAXSPAN;
-    static constexpr int TAUN = T::NM > 0 ? (TZ + 1 > NTL * ND ? TZ + 1 : NTL * ND) : NTL * ND;
+    static constexpr int TAUN = TZ + 1 > NTL * ND ? TZ + 1 : NTL * ND;
     static constexpr int TAU = U;
     static constexpr int CJ = TAU + TAUN;        /* phases 2-3: [NS][CJN] contact slots             */
     static constexpr int OBS = U;                /* report: observation staging                     */
@@ -1339,23 +1340,13 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
             }
         });
     } else {
-        Real tau[ND];
-#pragma unroll
-        for (int d = 0; d < ND; ++d) tau[d] = 0;
+        /* coordinate actuators: one torque per slot, gathered the same way */
+        if (lane == 0) lds[LY::TAU + LY::TZ] = Real(0);
         sfor<0, MPL>([&](auto jI) {
             constexpr int j = decltype(jI)::value;
             const int m = mslot<T>(lane + j * G);
-            if (m < T::NA) {
-                const int ad = SM.act_dof[m];
-                const Real f = control[j] * SM.ca_opt[m];
-#pragma unroll
-                for (int d = 0; d < ND; ++d) tau[d] += (d == ad) ? f : Real(0);
-            }
+            if (m < T::NA) lds[LY::TAU + (lane + j * G) * T::MAXSPAN] = control[j] * SM.ca_opt[m];
         });
-        if (lane < LY::NTL) {
-#pragma unroll
-            for (int d = 0; d < ND; ++d) lds[LY::TAU + ND * lane + d] = tau[d];
-        }
     }
     STAMP(5);
     if (lane < T::NS) contact_lane<T, Real>(SM, lds, lane, h);
@@ -1395,13 +1386,8 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     if (lane < ND) {
         const Real *Sd = lds + LY::S + 6 * lane, *wb = lds + LY::WB + 6 * SM.dof_cb[lane];
         Real r = -(dot3(Sd, wb) + dot3(Sd + 3, wb + 3));
-        if constexpr (T::NM > 0) {
 #pragma unroll
-            for (int i = 0; i < T::MAXARM; ++i) r += lds[LY::TAU + SM.tau_src[lane][i]];
-        } else {
-#pragma unroll
-            for (int m = 0; m < LY::NTL; ++m) r += lds[LY::TAU + ND * m + lane];
-        }
+        for (int i = 0; i < T::MAXARM; ++i) r += lds[LY::TAU + SM.tau_src[lane][i]];
         Real Y[FT::N > 0 ? FT::N : 1][6];
 #pragma unroll
         for (int b = 0; b < FT::N; ++b)
@@ -2407,13 +2393,16 @@ template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, 
         for (int d = 0; d < SDim<T>::NDD; ++d)
             for (int i = 0; i < T::MAXARM; ++i) m.tau_src[d][i] = (uint8_t)LY::TZ;
         int cnt[SDim<T>::NDD] = {};
+        auto add = [&](int d, int slot) {
+            if (d >= 0 && d < T::ND && cnt[d] < T::MAXARM) m.tau_src[d][cnt[d]++] = (uint8_t)slot;
+        };
         for (int sl = 0; sl < LY::MPL * T::G; ++sl) {
             const int mi = (T::NM > T::G && sl < T::NM) ? T::mperm[sl] : sl;
-            if (mi >= p.nmuscle) continue;
-            for (int k = 0; k < m.mus[mi].nspan; ++k) {
-                const int d = m.mus[mi].span[k];
-                if (cnt[d] < T::MAXARM) m.tau_src[d][cnt[d]] = (uint8_t)(sl * T::MAXSPAN + k);
-                ++cnt[d];
+            if constexpr (T::NM > 0) {
+                if (mi < p.nmuscle)
+                    for (int k = 0; k < m.mus[mi].nspan; ++k) add(m.mus[mi].span[k], sl * T::MAXSPAN + k);
+            } else {
+                if (mi < T::NA) add(T::act_dof[mi], sl * T::MAXSPAN);
             }
         }
     }
@@ -2578,10 +2567,14 @@ template <class T> bool topology_matches(const bioim_modelpack_t &p) {
         if (p.osbody[b].cbody != T::os_cb[b]) return false;
     for (int l = 0; l < T::NL; ++l)
         if (p.limit[l].dof != T::limit_dof[l] || p.limit[l].coord != T::limit_coord[l]) return false;
-    if (p.nmuscle == 0)
-        for (int a = 0; a < T::NA; ++a)
+    if (p.nmuscle == 0) {
+        int arms[32] = {};
+        for (int a = 0; a < T::NA; ++a) {
             if (p.coordact[a].dof != T::act_dof[a] || p.pd_coord[a] != T::pd_coord[a] || p.pd_vcoord[a] != T::pd_vcoord[a])
                 return false;
+            if (T::act_dof[a] >= 0 && ++arms[T::act_dof[a]] > T::MAXARM) return false;
+        }
+    }
     for (int b = 0; b < T::NOBP; ++b)
         if (p.obs_bpos[b] != T::obs_bpos[b]) return false;
     for (int b = 0; b < T::NOBV; ++b)

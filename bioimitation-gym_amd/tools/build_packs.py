@@ -161,9 +161,13 @@ def emit_topology(struct, pk, lanes):  # noqa: C901
         maxspan = max(maxspan, bin(u & ~root).count('1'))
         for d in range(nd):
             arms[d] += (u & ~root) >> d & 1
+    if pk.nmuscle == 0:
+        for a in range(pk.nact):
+            if pk.coordact[a].dof >= 0:
+                arms[pk.coordact[a].dof] += 1
     s += f'    static constexpr int MAXPT = {maxpt}; /* path points per muscle (max) */\n'
     s += f'    static constexpr int MAXSPAN = {maxspan}; /* non-root dofs a muscle path moves (max) */\n'
-    s += f'    static constexpr int MAXARM = {max(arms + [1])}; /* muscles spanning one dof (max) */\n'
+    s += f'    static constexpr int MAXARM = {max(arms + [1])}; /* muscles (actuators) acting on one dof (max) */\n'
     # muscle slot -> muscle: when muscles take two passes over the lanes (NM > G), the second,
     # partly idle pass gets the cheapest paths (fewest points, no moving/conditional points)
     def cost(i):
