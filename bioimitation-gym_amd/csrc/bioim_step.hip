@@ -53,6 +53,7 @@ template <> struct Eps<float> {
     static constexpr float u_stop = 2e-7f;  /* Newton step after which the root is converged */
     static constexpr float v_tol = 1e-7f;   /* normalized velocity         */
     static constexpr float l_tol = 1e-9f;   /* fiber length (m)            */
+    static constexpr float l_stop = 1e-9f;  /* Newton step after which the length is converged */
     static constexpr int it_max = 24;
 };
 template <> struct Eps<double> {
@@ -62,6 +63,7 @@ template <> struct Eps<double> {
     static constexpr double u_stop = 1e-11;
     static constexpr double v_tol = 1e-15;
     static constexpr double l_tol = 1e-15;
+    static constexpr double l_stop = 1e-10;
     static constexpr int it_max = 60;
 };
 
@@ -1079,10 +1081,14 @@ DEV Real muscle_equilibrium(const SModel<T, Real> &SM, const SMuscle<Real> &mu, 
         Real dH = (a * dfal + dfpe) * mu.inv_lopt * cphi + (a * fal + fpe) * (w * w) / (l * l * sq) + dfse * mu.inv_lts / cphi;
         if (H > 0) hi = l; else lo = l;
         Real ln = l - H / dH;
-        if (!(ln >= lo && ln <= hi)) ln = Real(0.5) * (lo + hi);
+        const bool newton = ln >= lo && ln <= hi;
+        if (!newton) ln = Real(0.5) * (lo + hi);
         Real dl = fabs(ln - l);
         l = ln;
         if (dl <= Eps<Real>::l_tol || (it >= 1 && dl <= Real(1e3) * Eps<Real>::l_tol && dl >= Real(0.5) * dprev)) break;
+        /* a Newton step of at most l_stop leaves an error ~ |H''/2H'| l_stop^2,
+         * far below l_tol (as u_stop for the fiber velocity) */
+        if (newton && dl <= Eps<Real>::l_stop) break;
         dprev = dl;
     }
     return l;

@@ -23,7 +23,10 @@ import glob, json, os, sys, collections
 d = collections.defaultdict(list)
 for f in sorted(glob.glob(os.path.join(sys.argv[1], '*.json'))):
     tag, env, _ = os.path.basename(f).split('__')
-    d[(env, tag)].append(json.load(open(f))['roofline']['kernel_ms'])
+    j = json.load(open(f))
+    d[(env, tag)].append((j['roofline']['kernel_ms'], j.get('done_rate')))
 for (env, tag), v in sorted(d.items()):
-    print(f'{env:30s} {tag:22s} kernel ms ' + ' '.join(f'{x:.4f}' for x in v) + f'  min {min(v):.4f}')
+    ms = [x for x, _ in v]
+    print(f'{env:30s} {tag:22s} kernel ms ' + ' '.join(f'{x:.4f}' for x in ms) + f'  min {min(ms):.4f}'
+          f'  done_rate {v[0][1]}')
 PY
