@@ -488,9 +488,64 @@ def main_perturbations():
     print('wrote', path)
 
 
+CONFIG_CASES = [   # (env_id, module under envs/, class, config overrides) for tests/golden/config_switches.npz
+    ('MuscleWalkingImitation2D-v0', 'muscle.planar.muscle_walking_imitation_env2D', 'MuscleWalkingImitationEnv2D',
+     {'use_target_obs': False}),
+    ('MuscleWalkingImitation2D-v0', 'muscle.planar.muscle_walking_imitation_env2D', 'MuscleWalkingImitationEnv2D',
+     {'use_target_obs': False, 'use_GRF': False, 'horizon': 1}),
+    ('TorqueWalkingImitation2D-v0', 'torque.planar.torque_walking_imitation_env2D', 'TorqueWalkingImitationEnv2D',
+     {'use_target_obs': False, 'r_weights': [0.3, 0.5, 0.4], 'horizon': 8}),
+    ('TorqueWalkingImitation2D-v0', 'torque.planar.torque_walking_imitation_env2D', 'TorqueWalkingImitationEnv2D',
+     {'use_GRF': False, 'horizon': 2}),
+    ('MuscleRunningImitation3D-v0', 'muscle.spatial.muscle_running_imitation_env3D', 'MuscleRunningImitationEnv3D',
+     {'use_target_obs': False, 'r_weights': [0.6, 0.1, 0.4]}),
+    ('MuscleLockedKneeImitation3D-v0', 'muscle.spatial.muscle_locked_knee_imitation_env3D',
+     'MuscleLockedKneeImitationEnv3D', {'use_target_obs': False, 'use_GRF': False, 'horizon': 7}),
+    ('MusclePalsyImitation3D-v0', 'muscle.spatial.muscle_palsy_imitation_env3D', 'MusclePalsyImitationEnv3D',
+     {'use_target_obs': False, 'horizon': 4, 'r_weights': [0.2, 0.3, 0.5]}),
+    ('TorqueWalkingImitation3D-v0', 'torque.spatial.torque_walking_imitation_env3D', 'TorqueWalkingImitationEnv3D',
+     {'use_target_obs': False, 'horizon': 6}),
+]
+
+
+def main_configs():
+    """Config-switch episodes (tests/golden/config_switches.npz): use_target_obs
+    off, use_GRF off, horizons 1..8 and r_weights overrides, run by the
+    reference's own env classes (configs/env_default.py:7-15 keys)."""
+    out = {}
+    rng = np.random.Generator(np.random.PCG64(23))
+    for j, (env_id, modfile, cls, cfg) in enumerate(CONFIG_CASES):
+        config = dict(DEFAULT_CFG, **cfg)
+        env, pk = make_env(env_id, 'bioimitation.imitation_envs.envs.' + modfile, cls, config)
+        T = 16
+        if pk.nmuscle:
+            acts = rng.uniform(0.0, 0.5, size=(T, pk.nact))
+
+            def act(t, e, acts=acts):
+                return acts[t].copy()
+        else:
+            noise = rng.normal(0.0, 0.03, size=(T, pk.nact))
+            pdc = [CURRENT['names']['coords'][pk.pd_coord[i]] for i in range(pk.nact)]
+
+            def act(t, e, noise=noise, pdc=pdc):
+                row = e.q_d.iloc[min(e.osim_model.istep + 1, len(e.q_d) - 1)]
+                return np.array([row[c] for c in pdc]) + noise[t]
+        ep = run_episode(env, pk, 9000 + j, T, act, nan_at=(3,))
+        ep.update(config=repr(config), env_id=env_id)
+        out[f'ep{j}'] = ep
+        print(env_id, cfg, 'index', ep['index'], 'steps', len(ep['reward']), 'obs dim', ep['obs'].shape[1])
+    flat = {f'{k}_{f}': np.asarray(v) for k, ep in out.items() for f, v in ep.items()}
+    flat['n_episodes'] = np.array(len(out))
+    path = os.path.join(HERE, 'config_switches.npz')
+    np.savez_compressed(path, **flat)
+    print('wrote', path)
+
+
 def main():
     if '--perturbations' in sys.argv:
         return main_perturbations()
+    if '--configs' in sys.argv:
+        return main_configs()
     out = {}
     # ---------------- MuscleWalkingImitation2D-v0
     mod = 'bioimitation.imitation_envs.envs.muscle.planar.muscle_walking_imitation_env2D'

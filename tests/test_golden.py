@@ -68,6 +68,29 @@ def test_obs_layout_matches_reference_keys(env_id):
         assert d['phase'] == ep['obs0'][0] and len(d['coordinate_vel']) == pk.ncoord
 
 
+def test_oracle_matches_reference_config_switches(oracle_lib):
+    """tests/golden/config_switches.npz: use_target_obs off, use_GRF off,
+    horizons 1..8, r_weights overrides (configs/env_default.py:7-15), run by
+    the reference's own env classes; the oracle must reproduce every step."""
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(__file__)), 'tests/golden/config_switches.npz')
+    z = np.load(path, allow_pickle=False)
+    assert int(z['n_episodes']) >= 8
+    for j in range(int(z['n_episodes'])):
+        ep = {k[len(f'ep{j}_'):]: z[k] for k in z.files if k.startswith(f'ep{j}_')}
+        env_id, cfg = str(ep['env_id']), ast.literal_eval(str(ep['config']))
+        pk = load_pack(env_id, cfg)
+        assert pk.obs_dim == ep['obs'].shape[1], (env_id, cfg)
+        orc = oracle_lib.Oracle(pk)
+        buf = orc.new_envs(1)
+        np.testing.assert_allclose(orc.reset(buf, 0, int(ep['index'])), ep['obs0'], rtol=1e-12, atol=1e-12)
+        for t in range(len(ep['reward'])):
+            o, r, d, info = orc.step(buf, 0, ep['actions'][t])
+            np.testing.assert_allclose(o, ep['obs'][t], rtol=1e-11, atol=1e-11, err_msg=f'{env_id} {cfg} step {t}')
+            assert abs(r - ep['reward'][t]) < 1e-11 and d == bool(ep['done'][t])
+            np.testing.assert_allclose(info, ep['info'][t], rtol=1e-11, atol=1e-12)
+
+
 def test_perturbation_schedule_and_episodes(oracle_lib):
     """apply_perturbations (muscle_walking_imitation_env2D.py:83-100): the
     reference's own construction (np.random seeded) drew the push schedule

@@ -1,0 +1,149 @@
+"""HIP path vs the reference's own env code, directly (no oracle in between),
+and the HIP path at the metric's full grid size.
+
+1. Golden replay.  Every episode in tests/golden/*.npz was produced by the
+   reference's env classes (tests/golden/make_golden.py): reset index, raw
+   actions (NaNs included), obs, reward, done and all_rewards per step, for
+   every built ID and the config switches the fixtures cover (horizon 1..8,
+   use_GRF off, use_target_obs off, r_weights overrides, mode='test',
+   chained episodes that keep old_pos_pelvisx and the deque, perturbation
+   pushes).  Here each episode is replayed through the reference-shaped
+   single-env API (bioimitation.envs.make -> VectorEnv -> libbioim.so) with
+   the reset index chosen the way the reference chooses it
+   (random.randint after random.seed, muscle_walking_imitation_env2D.py:144)
+   and compared to the fixture: relative error (to max(|x|, 1)) below 1e-9
+   on obs, reward and all_rewards, done equal.  The fixture physics is the
+   fp64 oracle's; GPU and oracle differ only in operation order.
+
+2. Full size.  4096 envs (256 workgroups, the BASELINE config) of Muscle2D,
+   Torque2D and Running3D for 12 steps, auto-reset off; a strided subset of
+   >= 128 envs that includes the first and last workgroup (envs 0..15 and
+   4080..4095) is compared to the oracle at 1e-6 (observed ~1e-9).
+"""
+import ast
+import glob
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN_FILES = sorted(glob.glob(os.path.join(HERE, 'golden', '*.npz')))
+TOL = 1e-9
+
+
+def _episodes(path):
+    z = np.load(path, allow_pickle=False)
+    stem = os.path.basename(path)[:-4]
+    for i in range(int(z['n_episodes'])):
+        ep = {k[len(f'ep{i}_'):]: z[k] for k in z.files if k.startswith(f'ep{i}_')}
+        ep.setdefault('env_id', np.array(stem))
+        yield ep
+
+
+def _seed_for_index(index, hi):
+    for s in range(1_000_000):
+        random.seed(s)
+        if random.randint(0, hi) == index:
+            random.seed(s)
+            return s
+    raise RuntimeError(index)
+
+
+def _rel(a, b):
+    return np.abs(np.asarray(a, dtype=np.float64) - b) / np.maximum(1.0, np.abs(b))
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+@pytest.mark.parametrize('path', GOLDEN_FILES, ids=[os.path.basename(p)[:-4] for p in GOLDEN_FILES])
+def test_golden_replay_on_hip_path(path):
+    from bioimitation import envs
+    worst, nsteps, env, key = 0.0, 0, None, None
+    for ep in _episodes(path):
+        env_id = str(ep['env_id'])
+        cfg = ast.literal_eval(str(ep['config']))
+        chained = 'chained' in ep
+        if not chained or env is None or key != (env_id, repr(cfg)):
+            assert not chained, 'a chained episode follows its predecessor on the same env'
+            if env is not None:
+                env.close()
+            if cfg.get('apply_perturbations'):
+                np.random.seed(int(ep['np_seed']))      # the reference draws its push schedule at construction
+            env = envs.make(env_id, cfg)
+            key = (env_id, repr(cfg))
+        index = int(ep['index'])
+        if cfg.get('mode') == 'test':
+            assert index == 0
+        else:
+            _seed_for_index(index, env._env.pack.reset_hi)
+        obs0 = env.reset()
+        e = _rel(obs0, ep['obs0']).max()
+        assert e < TOL, (env_id, cfg, 'reset', e)
+        for t in range(len(ep['reward'])):
+            o, r, d, info = env.step(ep['actions'][t])
+            e = max(_rel(o, ep['obs'][t]).max(), _rel(r, ep['reward'][t]),
+                    _rel(info['all_rewards'], ep['info'][t]).max())
+            assert e < TOL, (env_id, cfg, t, e)
+            assert d == bool(ep['done'][t]), (env_id, cfg, t)
+            assert isinstance(r, float) and isinstance(d, bool) and len(info['all_rewards']) == ep['info'].shape[1]
+            worst = max(worst, e)
+            nsteps += 1
+    env.close()
+    print(f'{os.path.basename(path)}: {nsteps} reference steps replayed on the HIP path, max rel err {worst:.2e}')
+
+
+FULL_IDS = ['MuscleWalkingImitation2D-v0', 'TorqueWalkingImitation2D-v0', 'MuscleRunningImitation3D-v0']
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+@pytest.mark.parametrize('env_id', FULL_IDS)
+def test_full_grid_4096_envs_vs_oracle(env_id):
+    import torch
+    import oracle
+    from bioimitation.registry import load_pack
+    from bioimitation.vector_env import VectorEnv
+    n, T = 4096, 12
+    pk = load_pack(env_id)
+    env = VectorEnv(env_id, n, precision=64, seed=5, auto_reset=False)
+    assert env.launch['workgroups'] == n // env.launch['envs_per_workgroup'] == 256
+    rng = np.random.default_rng(44)
+    rows = rng.integers(0, pk.reset_hi + 1, size=n)
+    env.reset(ref_index=rows)
+    epw = env.launch['envs_per_workgroup']
+    check = np.unique(np.concatenate([np.arange(epw), np.arange(n - epw, n), np.arange(epw, n - epw, 37),
+                                      [2047, 2048]]))
+    assert len(check) >= 128
+    orc = oracle.Oracle(pk)
+    bufs = orc.new_envs(len(check))
+    for j, i in enumerate(check):
+        orc.reset(bufs, j, int(rows[i]))
+    alive = np.ones(len(check), bool)
+    worst = 0.0
+    for t in range(T):
+        if pk.nmuscle:
+            acts = rng.uniform(0.0, 1.0, size=(n, pk.nact))
+        else:
+            st = env.get_state()[:, 1].astype(int) + 1
+            acts = np.array([[pk.ref_q[min(r, pk.nrows - 1)][pk.pd_coord[a]] for a in range(pk.nact)] for r in st])
+            acts += rng.normal(0.0, 0.05, size=acts.shape)
+        obs, rew, done, info = env.step(torch.as_tensor(acts, device=env.device))
+        torch.cuda.synchronize()
+        obs, rew, done, info = (x.cpu().numpy() for x in (obs, rew, done, info))
+        assert np.isfinite(obs).all()
+        for j, i in enumerate(check):
+            if not alive[j]:
+                continue
+            o, r, d, inf = orc.step(bufs, j, acts[i])
+            e = max(_rel(obs[i], o).max(), abs(rew[i] - r), _rel(info[i], inf).max())
+            assert e < 1e-6, (t, i, e)
+            assert bool(done[i]) == d, (t, i)
+            worst = max(worst, e)
+            alive[j] = not d
+    print(f'{env_id} 4096 envs x {T} steps: {len(check)} envs checked (first/last workgroup included), '
+          f'max rel err {worst:.2e}, alive {alive.sum()}/{len(check)}')
+    env.close()

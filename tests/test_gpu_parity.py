@@ -408,4 +408,48 @@ def test_parity_200_identical_action_steps(env_id):
             alive[i] = not d
     print(f'{env_id} 200-step parity: max rel err {worst:.2e}; steps lived min/median/max '
           f'{lived.min()}/{int(np.median(lived))}/{lived.max()}, alive at the end {alive.sum()}/{n}')
+    # the drive is open loop (the reference's PD gains, Kp = 100 N m/rad, cannot hold the
+    # model up without a learned policy), so episodes end well before t = 200; the oracle run
+    # of this exact drive gives the lived-step counts asserted here (tools/survival_probe.py)
+    assert lived.sum() >= {'MuscleWalkingImitation2D-v0': 1900, 'TorqueWalkingImitation2D-v0': 2050,
+                           'MuscleRunningImitation3D-v0': 1800}[env_id], lived
+    env.close()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+@pytest.mark.parametrize('env_id', ['MuscleWalkingImitation2D-v0', 'TorqueWalkingImitation2D-v0',
+                                    'MuscleRunningImitation3D-v0', 'MusclePalsyImitation3D-v0'])
+def test_parity_200_steps_through_termination(env_id):
+    """The 200-step horizon in full: every env is stepped 200 times with the
+    same actions on both sides and `done` is only compared, never acted on
+    (the reference's env keeps integrating when step() is called after done:
+    OsimEnv.step, opensim_environment.py:100-113, has no done guard).  So
+    the trajectories run through falls, ground impacts and lying contact,
+    the stiffest part of the model.  Reset rows leave 200 reference rows
+    after the start (istep + 1 stays inside the table).  Bound: obs and
+    reward within 1e-4 relative (north_star), on every env and every step."""
+    import torch
+    rng = np.random.default_rng(201)
+    n, T = 32, 200
+    pk, env, orc, bufs = _setup(env_id, n, 64)
+    rows = rng.integers(0, min(pk.reset_hi, pk.nrows - T - 2) + 1, size=n)
+    env.reset(ref_index=rows)
+    for i in range(n):
+        orc.reset(bufs, i, int(rows[i]))
+    worst = np.zeros(T)
+    ever_done = np.zeros(n, bool)
+    for t in range(T):
+        acts = rng.uniform(0.0, 0.4, size=(n, env.action_dim)) if 'Muscle' in env_id else \
+            _actions(env_id, rng, n, env.action_dim, pk, rows + t + 1)
+        obs, rew, done, _ = env.step(torch.as_tensor(acts, device=env.device))
+        torch.cuda.synchronize()
+        obs, rew, done = (v.cpu().numpy() for v in (obs, rew, done))
+        for i in range(n):
+            o, r, d, _ = orc.step(bufs, i, acts[i])
+            worst[t] = max(worst[t], _rel(obs[i], o).max(), abs(rew[i] - r) / max(1.0, abs(r)))
+            assert bool(done[i]) == d, (t, i)
+            ever_done[i] |= d
+    print(f'{env_id} 200 steps through termination: max rel err at t=1/50/100/200 '
+          f'{worst[0]:.1e}/{worst[49]:.1e}/{worst[99]:.1e}/{worst[-1]:.1e}; {ever_done.sum()}/{n} envs terminated')
+    assert worst.max() < 1e-4, (int(worst.argmax()), worst.max())
     env.close()
