@@ -2,26 +2,38 @@
 4096 envs per GPU (BASELINE.json metric), one process per GPU.
 
     python bench.py [--gpus N --steps K --warmup W --envs 4096 --precision 64]
-    (N > 1: launched by torch.distributed.run; RANK/LOCAL_RANK/WORLD_SIZE)
+
+N > 1: the driver launches N ranks with torch.distributed.run (RANK /
+LOCAL_RANK / WORLD_SIZE set).  Run directly with --gpus N > 1, bench.py starts
+that launcher itself as a child process, before anything touches a GPU, and
+exits with its status; a WORLD_SIZE that disagrees with --gpus, or fewer
+visible GPUs than ranks, is refused with a non-zero exit (never a silent
+1-GPU number).
 
 A "step" = one batched env step of every env on every rank (one kernel
 launch per GPU): action pre-processing, nsub semi-implicit substeps of the
 musculoskeletal dynamics, realize, obs/reward/done, in-kernel auto-reset.
 Actions: PCG64(seed=rank) U[0,1] excitations generated on the host and
-uploaded once before timing; inputs resident in HBM.
+uploaded once before timing; inputs resident in HBM.  An
+untimed burn-in (default 150 steps) first brings the batch to its
+steady-state termination rate; the done rate reported is the one of the
+timed steps themselves (device reset counters read before and after).
 Environments shard by index across ranks (no data-path collective), so
 scaling is weak: per-GPU work is fixed.
 """
 import argparse
 import json
+import math
 import os
+import subprocess
 import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(REPO, 'bioimitation-gym_amd'), os.path.join(REPO, 'oracle')]
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_VEC_PEAK_TF = 78.6    # 256 CU x 4 SIMD x 16 fp64 FMA lanes/clk x 2 flop x 2.4 GHz
 
 
 def algorithmic_bytes_per_env_step(pk, real_bytes):
@@ -34,29 +46,86 @@ def algorithmic_bytes_per_env_step(pk, real_bytes):
     return 2 * state_bytes + io
 
 
-def cpu_baseline(env_id, seconds=12.0):
-    """fp64 C oracle (oracle/, a port of the step) on host threads, bounded sample."""
+def host_cores():
+    """CPUs this process may run on: affinity mask, capped by a cgroup v2 CPU
+    quota when one is set (the GPU box grants a share of a larger machine)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open('/sys/fs/cgroup/cpu.max').read().split()
+        if quota != 'max':
+            n = min(n, max(1, math.ceil(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def _cpu_rate(env_id, threads, seconds, n_per_thread=64):
+    """fp64 C oracle (oracle/, a port of the step): env-steps/s of a batch of
+    n_per_thread x threads envs, auto-reset on the host, bounded sample."""
     import numpy as np
     import oracle
     from bioimitation.registry import load_pack
     pk = load_pack(env_id)
     orc = oracle.Oracle(pk)
-    threads = min(16, os.cpu_count() or 1)
-    n = 64 * threads
+    n = n_per_thread * threads
     bufs = orc.new_envs(n)
     rng = np.random.Generator(np.random.PCG64(0))
     for i in range(n):
         orc.reset(bufs, i, int(rng.integers(0, pk.reset_hi + 1)))
     steps, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        acts = rng.uniform(0, 1, size=(n, pk.nact))
+        if pk.nmuscle:
+            acts = rng.uniform(0, 1, size=(n, pk.nact))
+        else:   # PD targets at the reference (SURVEY.md 8d)
+            acts = np.tile([pk.ref_q[min(int(pk.reset_hi), pk.nrows - 1)][pk.pd_coord[a]] for a in range(pk.nact)],
+                           (n, 1)) + rng.normal(0, 0.05, size=(n, pk.nact))
         _, _, done, _ = orc.batch_step(bufs, n, acts, nthreads=threads, want_obs=True)
         for i in np.nonzero(done)[0]:
             orc.reset(bufs, int(i), int(rng.integers(0, pk.reset_hi + 1)))
         steps += 1
     dt = time.perf_counter() - t0
-    return {'value': n * steps / dt, 'unit': 'env-steps/s', 'cores': threads, 'kind': 'port',
-            'sample': f'{n} envs x {steps} steps ({dt:.1f} s), fp64 C oracle, {threads} threads, auto-reset on host'}
+    return n * steps / dt, f'{n} envs x {steps} steps ({dt:.1f} s)'
+
+
+def cpu_baseline(env_id, seconds=12.0):
+    """the fp64 CPU restatement on the GPU box's host cores,
+    same run.  The headline config on every usable core, plus C1 (1 env, 1
+    thread, us/step), C2 (Torque2D) and C4 (Running3D) batch rates."""
+    cores = host_cores()
+    value, sample = _cpu_rate(env_id, cores, seconds)
+    extra = {}
+    r1, s1 = _cpu_rate('TorqueWalkingImitation2D-v0', 1, 2.0, n_per_thread=1)
+    extra['C1_TorqueWalkingImitation2D_1env_1thread'] = {'us_per_step': 1e6 / r1, 'sample': s1}
+    for tag, eid in (('C2', 'TorqueWalkingImitation2D-v0'), ('C4', 'MuscleRunningImitation3D-v0')):
+        if eid != env_id:
+            r, s = _cpu_rate(eid, cores, 3.0)
+            extra[f'{tag}_{eid[:-3]}'] = {'value': r, 'unit': 'env-steps/s', 'cores': cores, 'sample': s}
+    return {'value': value, 'unit': 'env-steps/s', 'cores': cores, 'kind': 'port',
+            'sample': f'{sample}, {env_id}, fp64 C oracle (CPU restatement, not OpenSim), {cores} threads = '
+                      f'the CPUs this process may use (affinity, cgroup quota), auto-reset on host',
+            'configs': extra}
+
+
+def _profile_record(name, key):
+    path = os.path.join(REPO, 'profiles', name)
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path)).get(key)
+    except (OSError, ValueError):
+        return None
+
+
+def _spawn_ranks(a):
+    """`bench.py --gpus N` run directly: start torch.distributed.run as a child
+    (nothing in this process has touched a GPU) and return its exit status."""
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={a.gpus}',
+           '--master-addr', '127.0.0.1', f'--master-port={port}', os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ))
 
 
 def main():
@@ -64,6 +133,8 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=200)
     ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--burn-in', type=int, default=150,
+                    help='untimed steps before the warmup, to reach the steady-state termination rate')
     ap.add_argument('--envs', type=int, default=4096, help='envs per GPU')
     ap.add_argument('--precision', type=int, default=int(os.environ.get('BIOIM_PRECISION', 64)))
     ap.add_argument('--env-id', default='MuscleWalkingImitation2D-v0')
@@ -73,11 +144,21 @@ def main():
                          "MuscleLockedKneeImitation3D-v0,MusclePalsyImitation3D-v0")
     a = ap.parse_args()
 
+    if 'WORLD_SIZE' not in os.environ and a.gpus > 1:
+        sys.exit(_spawn_ranks(a))
+    world = int(os.environ.get('WORLD_SIZE', 1))
+    if world != a.gpus:
+        print(f'bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; refusing to report a mismatched n_gpus',
+              file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get('RANK', 0))
+    local = int(os.environ.get('LOCAL_RANK', 0))
+
     import numpy as np
     import torch
-    rank = int(os.environ.get('RANK', 0))
-    world = int(os.environ.get('WORLD_SIZE', 1))
-    local = int(os.environ.get('LOCAL_RANK', 0))
+    if local >= torch.cuda.device_count():
+        print(f'bench.py: rank {rank} needs GPU {local} but {torch.cuda.device_count()} are visible', file=sys.stderr)
+        sys.exit(2)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -96,18 +177,21 @@ def main():
         env.launch = {e.env_id: e.launch for e in env.envs}
         a.env_id = '+'.join(ids)
         a.no_cpu_baseline = True
+        handles = env.envs
     else:
         env = VectorEnv(a.env_id, a.envs, device=local, precision=a.precision, seed=1000, auto_reset=True,
                         env_offset=rank * a.envs)        # global env index block (bioimitation/parallel.py)
+        handles = [env]
     n, A = a.envs, env.action_dim
-    total = a.warmup + a.steps
+    pool = 64      # action batches cycled through (uploaded once; inputs resident in HBM)
     gen = np.random.Generator(np.random.PCG64(rank))
-    acts = torch.as_tensor(gen.uniform(0.0, 1.0, size=(total, n, A)), dtype=env.dtype, device=dev)
+    acts = torch.as_tensor(gen.uniform(0.0, 1.0, size=(pool, n, A)), dtype=env.dtype, device=dev)
     env.reset()
     stream = torch.cuda.current_stream(dev)
-    for k in range(a.warmup):
-        env.step(acts[k])
+    for k in range(a.burn_in + a.warmup):
+        env.step(acts[k % pool])
     torch.cuda.synchronize(dev)
+    resets0 = sum(h.reset_count() for h in handles)
 
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
@@ -115,8 +199,8 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for k in range(a.warmup, total):
-        env.step(acts[k])
+    for k in range(a.steps):
+        env.step(acts[(a.burn_in + a.warmup + k) % pool])
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
@@ -128,15 +212,9 @@ def main():
         tt = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt[0])
+    done_rate = (sum(h.reset_count() for h in handles) - resets0) / (n * a.steps)
     steps_total = world * n * a.steps
     value = steps_total / t_max
-    # done rate: an untimed pass over the same actions after the
-    # timed region, counting terminations on the device
-    dones = torch.zeros((), dtype=torch.float64, device=dev)
-    for k in range(a.warmup, total):
-        done = env.step(acts[k])[2]
-        dones += done.to(torch.float64).sum()
-    done_rate = float(dones) / (n * a.steps)
     if rank == 0:
         real_bytes = 8 if a.precision == 64 else 4
         if a.mixed:   # env-weighted mean over the segments
@@ -144,28 +222,30 @@ def main():
         else:
             B = algorithmic_bytes_per_env_step(env.pack, real_bytes)
         achieved = B * n / (kernel_ms * 1e-3) / 1e9
-        traffic = None
-        tf = os.path.join(REPO, 'profiles', 'traffic.json')
-        if os.path.exists(tf):
-            try:
-                rec = json.load(open(tf)).get(f'{a.env_id}/fp{a.precision}/{n}')
-                traffic = rec['bytes'] if rec else None    # rocprofv3 FETCH_SIZE + WRITE_SIZE per launch
-            except Exception:
-                traffic = None
+        key = f'{a.env_id}/fp{a.precision}/{n}'
+        tr = _profile_record('traffic.json', key)
+        traffic = tr['bytes'] if tr else None          # rocprofv3 2 x FETCH_SIZE + WRITE_SIZE per launch
+        roofline = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                    'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                    'traffic_over_algorithmic': traffic / (B * n) if traffic else None,
+                    'bytes_per_env_step': B, 'kernel_ms': kernel_ms}
+        if tr:
+            roofline['traffic_source'] = tr.get('source')
         line = {
             'metric': 'env steps/sec (whole node), MuscleWalkingImitation2D-v0 @ 4096 envs/GPU'
             if a.env_id == 'MuscleWalkingImitation2D-v0' and n == 4096 else f'env steps/sec, {a.env_id} @ {n} envs/GPU',
             'value': value, 'unit': 'env-steps/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
-            'ms_per_step': t_max / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+            'burn_in': a.burn_in, 'ms_per_step': t_max / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': f'f{a.precision}', 'done_rate': done_rate,
             'data': 'synthetic: PCG64 U[0,1] muscle excitations; reference motion synthesized from the shipped 3D IK',
             'config': {'workload': f'{a.env_id} batched env.step, {n} envs/GPU, nsub={env.nsub}, auto-reset',
                        'envs_per_gpu': n, 'lanes_per_env': env.lanes_per_env, 'parallelism': f'env-shard x{world}',
                        'launch': env.launch},
-            'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                         'bytes_per_env_step': B, 'kernel_ms': kernel_ms},
+            'roofline': roofline,
         }
+        valu = _profile_record('valu.json', key)
+        if valu:   # the bound that is live for this kernel, from the rocprofv3 SQ passes
+            line['valu'] = valu
         if not a.no_cpu_baseline and world == 1:
             line['cpu_baseline'] = cpu_baseline(a.env_id)
         print(json.dumps(line), flush=True)

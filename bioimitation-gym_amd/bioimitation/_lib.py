@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get('BIOIM_LIB', os.path.join(PKG_ROOT, 'build', 'libbioim
 
 EXPORTS = ['bioim_create', 'bioim_destroy', 'bioim_reset', 'bioim_step', 'bioim_set_auto_reset', 'bioim_set_env_offset', 'bioim_set_io_strides', 'bioim_step_group', 'bioim_set_perturbation', 'bioim_id_eval', 'bioim_state_dim',
            'bioim_get_state', 'bioim_set_state', 'bioim_query', 'bioim_query_launch', 'bioim_stream', 'bioim_set_stream', 'bioim_sync',
-           'bioim_last_error', 'bioim_modelpack_size']
+           'bioim_last_error', 'bioim_modelpack_size', 'bioim_build_id', 'bioim_reset_count', 'bioim_set_final_obs']
 
 _lib = None
 
@@ -55,14 +55,31 @@ def load():
         'bioim_sync': (C.c_int, [vp]),
         'bioim_last_error': (C.c_char_p, []),
         'bioim_modelpack_size': (C.c_uint64, []),
+        'bioim_build_id': (C.c_char_p, []),
+        'bioim_reset_count': (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+        'bioim_set_final_obs': (C.c_int, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
         f.restype, f.argtypes = res, args
     if L.bioim_modelpack_size() != C.sizeof(P.ModelPack):
         raise BioimError('ModelPack layout mismatch between libbioim.so and packdef.py')
+    check_build_id(L)
     _lib = L
     return L
+
+
+def check_build_id(L):
+    """A library built from other sources or flags than the tree it sits in
+    is refused (set BIOIM_LIB to load a variant build on purpose)."""
+    from . import _buildinfo
+    if 'BIOIM_LIB' in os.environ:
+        return
+    got = L.bioim_build_id().decode()
+    want = _buildinfo.build_id()
+    if got != want:
+        raise BioimError(f'{LIB_PATH} was built from other sources/flags (build id {got}, tree {want}); '
+                         'run __graft_entry__.build()')
 
 
 def check(rc):

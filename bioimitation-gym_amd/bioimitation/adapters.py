@@ -13,7 +13,9 @@ Neither ray nor gym is importable here, so the adapters are duck-typed:
   in-kernel auto-reset is off.
 - :class:`GymVectorEnv` — gym's vector-env convention (batched ``reset`` /
   ``step``, finished envs reset automatically and report their reset
-  observation): in-kernel auto-reset on.
+  observation, the terminal one in ``infos['final_observation']``): in-kernel
+  auto-reset on.  Outputs are fresh tensors (the env's own buffers are
+  overwritten by the next launch), so a replay loop may keep them.
 - :class:`MeanStdFilter` — RLlib's ``MeanStdFilter`` (demean, destd,
   clip 10) as a running mean/variance kept on the GPU and updated from whole
   batches, so normalised observations never leave the device.
@@ -144,27 +146,36 @@ class RLlibVectorEnv:
 class GymVectorEnv:
     """gym vector-env convention on the device: ``reset() -> obs (N, O)``,
     ``step(actions) -> (obs, rewards, dones, infos)`` with finished envs reset
-    in the same kernel launch (their obs row is the post-reset observation).
+    in the same kernel launch (their obs row is the post-reset observation;
+    ``infos['final_observation']`` holds every env's observation from before
+    the reset, i.e. the terminal observation of the done rows, and
+    ``infos['_final_observation']`` marks those rows).  Returned tensors are
+    copies, safe to store in a replay buffer across steps.
     ``normalize=True`` applies a device :class:`MeanStdFilter` to the
-    observations (RLlib's ``observation_filter``)."""
+    observations (RLlib's ``observation_filter``); the final observations are
+    normalised with the same statistics, without updating them."""
 
     def __init__(self, env_id: str, num_envs: int, config: dict = None, device: int = 0, precision: int = 64,
                  seed: int = 0, env_offset: int = 0, normalize: bool = False):
         self.env = VectorEnv(env_id, num_envs, config=config, device=device, precision=precision, seed=seed,
                              auto_reset=True, env_offset=env_offset)
+        self.env.enable_final_obs()
         self.num_envs = num_envs
         self.single_observation_space, self.single_action_space = _spaces(self.env)
         self.filter = MeanStdFilter(self.env.obs_dim, device=self.env.device) if normalize else None
 
-    def _obs(self, obs):
-        return self.filter(obs) if self.filter is not None else obs
+    def _obs(self, obs, update=True):
+        return self.filter(obs, update=update) if self.filter is not None else obs.clone()
 
     def reset(self):
         return self._obs(self.env.reset())
 
     def step(self, actions):
         obs, rew, done, info = self.env.step(actions)
-        return self._obs(obs), rew, done.bool(), {'all_rewards': info}
+        d = done.bool()
+        infos = {'all_rewards': info.clone(), 'final_observation': self._obs(self.env.final_obs, update=False),
+                 '_final_observation': d.clone()}
+        return self._obs(obs), rew.clone(), d, infos
 
     def close(self):
         self.env.close()

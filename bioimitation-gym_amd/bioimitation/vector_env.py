@@ -4,8 +4,17 @@ one GPU, stepped by one kernel launch.
 This is the throughput surface (RLlib ``VectorEnv`` / gym vector-env shaped);
 :class:`bioimitation.envs.ImitationEnv` is the single-instance, reference-
 shaped surface built on top of it.  Buffers are torch tensors on the GPU;
-the kernel runs on torch's current stream of that device so it orders with
-the caller's torch work.
+each launch runs on torch's *current* stream of that device at the time of
+the call (the handle is re-bound when the caller switches streams), so it
+orders with the caller's torch work.
+
+Aliasing: ``reset()`` and ``step()`` return the env's persistent output
+tensors (``self.obs``, ``self.reward``, ``self.done``, ``self.info``), which
+the next launch overwrites in place — zero-copy for callers that consume a
+step before issuing the next.  Keep a result across steps with ``.clone()``
+(the adapters in :mod:`bioimitation.adapters` do).  With auto-reset on, a
+done env's row holds its post-reset observation; ``enable_final_obs()``
+keeps the terminal one in ``self.final_obs``.
 """
 from __future__ import annotations
 
@@ -34,8 +43,8 @@ class VectorEnv:
         _lib.check(L.bioim_create(C.byref(self.pack), self.num_envs, device, precision, seed, C.byref(h)))
         self._h = h
         self._L = L
-        with torch.cuda.device(self.device):
-            _lib.check(L.bioim_set_stream(h, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+        self._stream = None
+        self._bind_stream()
         q = (C.c_int32 * 8)()
         _lib.check(L.bioim_query(h, q))
         self.obs_dim, self.action_dim, self.info_dim, self.lanes_per_env, self.nsub, self.state_dim = \
@@ -52,6 +61,7 @@ class VectorEnv:
         self.reward = torch.zeros(n, dtype=self.dtype, device=self.device)
         self.done = torch.zeros(n, dtype=torch.uint8, device=self.device)
         self.info = torch.zeros((n, self.info_dim), dtype=self.dtype, device=self.device)
+        self.final_obs = None
         self.perturbation = None
         if (config or {}).get('apply_perturbations'):
             from .perturb import batch_points
@@ -78,6 +88,26 @@ class VectorEnv:
         _lib.check(self._L.bioim_set_perturbation(self._h, ob, len(xt), xt.ctypes.data_as(dp), yt.ctypes.data_as(dp)))
         self.perturbation = (np.asarray(x, dtype=np.float64), yt)
 
+    def _bind_stream(self):
+        """Launch on torch's current stream of the env's device (re-bound
+        whenever the caller has switched streams since the last launch)."""
+        import torch
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        if s != self._stream:
+            _lib.check(self._L.bioim_set_stream(self._h, C.c_void_p(s)))
+            self._stream = s
+
+    def enable_final_obs(self, on: bool = True):
+        """Keep each step's observation from before an in-kernel auto-reset in
+        ``self.final_obs`` (N, O): a done env's terminal observation (gym's
+        ``final_observation``); equal to ``obs`` for envs that did not reset."""
+        import torch
+        if on and self.final_obs is None:
+            self.final_obs = torch.zeros_like(self.obs)
+        elif not on:
+            self.final_obs = None
+        _lib.check(self._L.bioim_set_final_obs(self._h, self._ptr(self.final_obs)))
+
     @staticmethod
     def _ptr(t):
         return C.c_void_p(t.data_ptr()) if t is not None else None
@@ -99,6 +129,7 @@ class VectorEnv:
             if ids is None:
                 ids = torch.arange(self.num_envs, dtype=torch.int32, device=self.device)
             assert rows.numel() == n
+        self._bind_stream()
         _lib.check(self._L.bioim_reset(self._h, self._ptr(ids), self._ptr(rows), n, self._ptr(self.obs)))
         return self.obs
 
@@ -108,6 +139,7 @@ class VectorEnv:
         if a.dtype != self.dtype or a.device != self.device or not a.is_contiguous():
             a = a.to(device=self.device, dtype=self.dtype).contiguous()
         assert a.shape == (self.num_envs, self.action_dim), a.shape
+        self._bind_stream()
         _lib.check(self._L.bioim_step(self._h, self._ptr(a), self._ptr(self.obs), self._ptr(self.reward),
                                       self._ptr(self.done), self._ptr(self.info)))
         return self.obs, self.reward, self.done, self.info
@@ -121,6 +153,12 @@ class VectorEnv:
         s = np.ascontiguousarray(s, dtype=np.float64)
         assert s.shape == (self.num_envs, self.state_dim)
         _lib.check(self._L.bioim_set_state(self._h, s.ctypes.data_as(C.POINTER(C.c_double))))
+
+    def reset_count(self) -> int:
+        """Resets so far over all envs (explicit + in-kernel auto-resets)."""
+        n = C.c_uint64()
+        _lib.check(self._L.bioim_reset_count(self._h, C.byref(n)))
+        return int(n.value)
 
     def sync(self):
         _lib.check(self._L.bioim_sync(self._h))
@@ -193,6 +231,7 @@ class MixedVectorEnv:
             a = a.to(device=self.device, dtype=self.dtype).contiguous()
         assert a.shape == (self.num_envs, self.action_dim), a.shape
         p = VectorEnv._ptr
+        self.envs[0]._bind_stream()      # segment 0 launches on it; the others fork from and join into it
         _lib.check(self._L.bioim_step_group(self._hs, len(self.envs), p(a), p(self.obs), p(self.reward),
                                             p(self.done), p(self.info)))
         return self.obs, self.reward, self.done, self.info

@@ -5,20 +5,25 @@
 // forward dynamics, the realize at the end state, and the observation,
 // reward and termination of the reference's task envs.
 //
-// Work decomposition (CDNA4, wave64): an environment is a group of G lanes
-// (G = 16 for the 2D models: 4 envs per wave, 16 per 256-thread workgroup).
-//   - the multibody part (kinematics, composite-rigid-body mass matrix,
-//     Newton-Euler bias, contact, limits, Cholesky) is computed redundantly
-//     by every lane of the group, fully unrolled against the compile-time
-//     topology (topologies.h) so all of it lives in VGPRs;
-//   - muscle m runs on lane m (path geometry, Millard damped equilibrium,
-//     activation), and the generalized forces are summed across the group
-//     with xor-shuffles;
-//   - body frames and coordinates that muscle lanes index at run time are
-//     staged in LDS (one region per env).
-// Model constants are wave-uniform (scalar loads); per-env state is SoA in
-// HBM (env index fastest).  Reference semantics: see oracle/bioim_oracle.c,
-// which this kernel must match (tests/test_gpu_parity.py).
+// Work decomposition (CDNA4, wave64): an environment is a
+// group of G = 16 lanes for every topology, 4 envs per wave, 16 envs per
+// 256-thread workgroup, one wave per SIMD.
+//   - lanes take roles per phase: composite body (joint kinematics, frame
+//     composition, inertias, subtree sums), dof (lane d owns coordinate d's
+//     value and speed in registers, M entries, rhs), muscle (path geometry,
+//     moment arms over its span, Millard damped equilibrium; lane l also
+//     takes muscle l + 16 where a topology has more than 16), contact sphere,
+//     limit force, report slot;
+//   - lanes of one env exchange data through its per-env LDS region (frames,
+//     Plücker columns, packed M, torque slots) with wave-scope fences: the env
+//     never leaves its wave; group sums are xor-butterflies (bitwise identical
+//     totals on every lane);
+//   - the tree-sparse LTL solve runs redundantly on every lane in registers;
+//   - the lane-indexed model image (muscles, path points, joints, splines,
+//     spheres) is staged into LDS once per workgroup; uniform constants and
+//     the reference-motion tables are scalar loads.
+// Per-env state is SoA in HBM (env index fastest).  Reference semantics: see
+// oracle/bioim_oracle.c, which this kernel must match (tests/test_gpu_*.py).
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -1776,6 +1781,7 @@ template <class T, typename Real> struct LaunchArgs {
     int act_stride, obs_stride, info_stride;
     const Real *actions;
     Real *obs, *reward, *info;
+    Real *final_obs;   /* optional: the step's observation before any auto-reset (row stride obs_stride) */
     uint8_t *done_out;
     const int32_t *env_ids, *ref_index;
     uint64_t seed;
@@ -2087,6 +2093,8 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         wave_sync();
         if (obs)
             for (int k = lane; k < M.obs_dim; k += G) obs[(size_t)env * a.obs_stride + k] = ob[k];
+        if (a.final_obs && !reported_reset)
+            for (int k = lane; k < M.obs_dim; k += G) a.final_obs[(size_t)env * a.obs_stride + k] = ob[k];
         wave_sync();
         if (reported_reset) break;
 
@@ -2639,6 +2647,7 @@ struct bioim_handle {
     void *dstate;       /* DState<Real> (host copy of pointers) */
     void *pert_x, *pert_y; /* apply_perturbations table: double [pert_n], Real [pert_n][n] */
     int pert_n, pert_ob;
+    void *final_obs;    /* caller's device buffer [n][obs_stride] or null (bioim_set_final_obs) */
     Ops ops;
     bioim_modelpack_t pack;
 };
@@ -2664,6 +2673,7 @@ LaunchArgs<T, Real> make_args(bioim_handle_t *h, int mode, const void *actions, 
     a.act_stride = h->act_stride; a.obs_stride = h->obs_stride; a.info_stride = h->info_stride;
     a.actions = reinterpret_cast<const Real *>(actions);
     a.obs = reinterpret_cast<Real *>(obs);
+    a.final_obs = mode == 0 ? reinterpret_cast<Real *>(h->final_obs) : nullptr;
     a.reward = reinterpret_cast<Real *>(reward);
     a.info = reinterpret_cast<Real *>(info);
     a.done_out = done;
@@ -2845,6 +2855,11 @@ thread_local std::string g_err;
 extern "C" {
 
 const char *bioim_last_error(void) { return g_err.c_str(); }
+#ifndef BIOIM_BUILD_ID
+#define BIOIM_BUILD_ID "unstamped"
+#endif
+/* sha256 of the kernel sources + hipcc flags (bioimitation/_buildinfo.py) */
+const char *bioim_build_id(void) { return BIOIM_BUILD_ID; }
 uint64_t bioim_modelpack_size(void) { return sizeof(bioim_modelpack_t); }
 
 int bioim_create(const bioim_modelpack_t *pack, int n_envs, int device, int precision, uint64_t seed,
@@ -2934,6 +2949,12 @@ int bioim_step(bioim_handle_t *h, const void *actions, void *obs, void *reward, 
 int bioim_set_auto_reset(bioim_handle_t *h, int on) {
     if (!h) return fail(BIOIM_E_ARG, "null handle");
     h->auto_reset = on ? 1 : 0;
+    return 0;
+}
+
+int bioim_set_final_obs(bioim_handle_t *h, void *final_obs) {
+    if (!h) return fail(BIOIM_E_ARG, "null handle");
+    h->final_obs = final_obs;
     return 0;
 }
 
@@ -3051,6 +3072,28 @@ int bioim_set_state(bioim_handle_t *h, const double *host_state) {
     if (!h || !host_state) return fail(BIOIM_E_ARG, "bioim_set_state: bad arguments");
     HIPCHK(hipSetDevice(h->device));
     return h->precision == 64 ? xfer_state<double>(h, nullptr, host_state) : xfer_state<float>(h, nullptr, host_state);
+}
+
+/* total resets (explicit + in-kernel auto-resets) over the handle's envs */
+int bioim_reset_count(bioim_handle_t *h, uint64_t *total) {
+    if (!h || !total) return fail(BIOIM_E_ARG, "bioim_reset_count: bad arguments");
+    HIPCHK(hipSetDevice(h->device));
+    std::vector<char> buf(h->state_bytes);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipStreamSynchronize(h->side));
+    HIPCHK(hipMemcpy(buf.data(), h->state_buf, h->state_bytes, hipMemcpyDeviceToHost));
+    uint64_t sum = 0;
+    if (h->precision == 64) {
+        DState<double> hs;
+        state_layout<double>(h, buf.data(), &hs);
+        for (int e = 0; e < h->n; ++e) sum += (uint32_t)hs.resets[e];
+    } else {
+        DState<float> hs;
+        state_layout<float>(h, buf.data(), &hs);
+        for (int e = 0; e < h->n; ++e) sum += (uint32_t)hs.resets[e];
+    }
+    *total = sum;
+    return 0;
 }
 
 int bioim_query(const bioim_handle_t *h, int32_t *out) {

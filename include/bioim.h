@@ -137,6 +137,18 @@ int bioim_state_dim(const bioim_handle_t *h);
 int bioim_get_state(bioim_handle_t *h, double *host_state /* [N][state_dim] */);
 int bioim_set_state(bioim_handle_t *h, const double *host_state);
 
+/* Optional terminal-observation output: when set (a device buffer with the
+ * handle's obs row stride), every step also writes each env's observation
+ * as computed by that step *before* an in-kernel auto-reset replaces it, so
+ * a done env's terminal observation survives (gym's final_observation;
+ * bootstrapping in the reference's jaxrl SAC loop,
+ * tests/sample_baselines_training.py:69-91).  NULL disables it. */
+int bioim_set_final_obs(bioim_handle_t *h, void *final_obs);
+/* Sum over the handle's envs of their reset counters (explicit resets and
+ * in-kernel auto-resets); synchronizes the handle's streams.  Lets a caller
+ * count terminations over a stretch of steps without touching the step
+ * launches (bench.py's done rate).  No reference counterpart. */
+int bioim_reset_count(bioim_handle_t *h, uint64_t *total);
 /* out[0..7] = n_envs, obs_dim, nact, info_dim, precision, lanes_per_env, nsub, state_dim */
 int bioim_query(const bioim_handle_t *h, int32_t *out);
 /* out[0..4] = lanes per env, threads per workgroup, envs per workgroup,
@@ -148,6 +160,11 @@ int bioim_sync(bioim_handle_t *h);
 const char *bioim_last_error(void);
 /* sizeof(bioim_modelpack_t) as compiled into the library (layout check). */
 uint64_t bioim_modelpack_size(void);
+/* Build id: sha256 (16 hex digits) over the kernel sources and hipcc flags the
+ * library was compiled from (bioimitation/_buildinfo.py); the Python host
+ * refuses a library whose id differs from its source tree's.  No reference
+ * counterpart (build hygiene). */
+const char *bioim_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -88,3 +88,72 @@ def test_gym_vector_env_autoreset_and_filter():
         assert torch.isfinite(obs).all() and obs.abs().max() <= 10.0
     assert venv.filter.n == 64 * 21
     venv.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+def test_gym_vector_env_final_observation_and_copies():
+    """Terminal observations survive the in-kernel auto-reset
+    (infos['final_observation'], bioim_set_final_obs), equal to what the same
+    env produces without auto-reset; outputs are copies, so a replay loop that
+    keeps (obs, next_obs) pairs sees distinct tensors."""
+    import torch
+    from bioimitation.adapters import GymVectorEnv
+    from bioimitation.vector_env import VectorEnv
+    env_id, n = 'MuscleWalkingImitation2D-v0', 48
+    venv = GymVectorEnv(env_id, n, seed=4)
+    ref = VectorEnv(env_id, n, seed=4, auto_reset=False)
+    venv.reset()
+    ref.reset()
+    st = venv.env.get_state()
+    st[:, 1] = venv.env.pack.n_episode - 1 - (np.arange(n) % 2)      # even envs end on step 1, odd envs on step 2
+    st[:, 0] = 0.01 * st[:, 1]
+    venv.env.set_state(st)
+    ref.set_state(st)
+    g = torch.Generator(device='cuda').manual_seed(1)
+    kept, live, ndone = [], torch.ones(n, dtype=torch.bool, device=ref.device), 0
+    for t in range(2):       # even envs end on step 1, odd envs on step 2
+        a = torch.rand((n, venv.env.action_dim), generator=g, device=ref.device, dtype=torch.float64)
+        obs, rew, done, info = venv.step(a)
+        ro, rr, rd, _ = ref.step(a)
+        kept.append(obs)
+        lv = live                                  # rows not yet auto-reset in venv: same trajectory as ref
+        assert torch.equal(done[lv], rd.bool()[lv]) and torch.equal(rew[lv], rr[lv])
+        assert torch.equal(info['final_observation'][lv], ro[lv]), t     # pre-reset obs
+        assert torch.equal(info['_final_observation'], done)
+        nd = lv & done
+        assert torch.equal(obs[lv & ~done], ro[lv & ~done])
+        assert nd.any() and not torch.equal(obs[nd], ro[nd])              # done rows hold the reset observation
+        assert torch.equal(done, torch.arange(n, device=ref.device) % 2 == t)
+        ndone += int(nd.sum())
+        live = live & ~done
+    assert ndone == n and not torch.equal(kept[0], kept[1])
+    venv.close()
+    ref.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+def test_launch_follows_the_callers_stream():
+    """A step issued under `with torch.cuda.stream(s)` runs on s (the handle
+    is re-bound), so work queued on s before it is ordered before it."""
+    import torch
+    from bioimitation.vector_env import VectorEnv
+    env_id, n = 'TorqueWalkingImitation2D-v0', 32
+    a_env, b_env = VectorEnv(env_id, n, seed=2), VectorEnv(env_id, n, seed=2)
+    a_env.reset()
+    b_env.reset()
+    s = torch.cuda.Stream()
+    acts = torch.zeros((n, 7), dtype=torch.float64, device=a_env.device)
+    with torch.cuda.stream(s):
+        big = torch.randn((4096, 4096), device=a_env.device)
+        for _ in range(4):
+            big = big @ big.T / 64.0                 # a slow producer on s
+        acts_s = acts + 0.1 + 0 * big[0, 0].clamp(-1, 1)   # the action depends on it
+        o_s = b_env.step(acts_s)[0].clone()
+        assert b_env._stream == s.cuda_stream
+    o = a_env.step(acts + 0.1)[0].clone()
+    torch.cuda.synchronize()
+    assert torch.equal(o, o_s)
+    a_env.close()
+    b_env.close()

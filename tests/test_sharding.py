@@ -77,3 +77,21 @@ def test_two_rank_gloo_sharding_is_bit_identical():
     single = _rollout(0, total)
     np.testing.assert_array_equal(gathered, single)
     assert tmax == 2.0
+
+
+def test_bench_refuses_mismatched_world_size():
+    """bench.py never reports an n_gpus it did not run: WORLD_SIZE != --gpus
+    and too few visible GPUs both exit non-zero (no GPU is touched here)."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE='1', RANK='0', LOCAL_RANK='0')
+    r = subprocess.run([sys.executable, os.path.join(repo, 'bench.py'), '--gpus', '2'], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and 'WORLD_SIZE=1' in r.stderr
+    import torch
+    if torch.cuda.device_count() == 0:
+        r = subprocess.run([sys.executable, os.path.join(repo, 'bench.py'), '--gpus', '1', '--no-cpu-baseline'],
+                           env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 2 and 'visible' in r.stderr

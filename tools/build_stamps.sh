@@ -3,5 +3,6 @@
 set -e
 cd "$(dirname "$0")/.."
 C=bioimitation-gym_amd/csrc
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DBIOIM_STAMPS -mllvm -amdgpu-sched-strategy=iterative-ilp -Iinclude -I$C -Wno-unused-result \
-    -Wno-unused-value -o bioimitation-gym_amd/build/libbioim_stamps.so $C/bioim_step.hip
+# the shipped library's flags (bioimitation/_buildinfo.py: one place for them)
+FLAGS=$(cd bioimitation-gym_amd && python3 -m bioimitation._buildinfo flags)
+hipcc $FLAGS -shared -DBIOIM_STAMPS -o bioimitation-gym_amd/build/libbioim_stamps.so $C/bioim_step.hip

@@ -1,7 +1,8 @@
 """Static instruction mix between consecutive s_memtime stamps of the
 diagnostic (-DBIOIM_STAMPS) build, for one kernel.
 
-    hipcc ... -DBIOIM_STAMPS --offload-device-only -S bioim_step.hip -o ks.s
+    hipcc $(cd bioimitation-gym_amd && python3 -m bioimitation._buildinfo flags) \
+        -DBIOIM_STAMPS --offload-device-only -S bioim_step.hip -o ks.s
     python tools/phase_isa.py ks.s MuscleWalkingImitation2D_v0dE
 """
 import collections

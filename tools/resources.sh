@@ -4,7 +4,9 @@
 #   bash tools/resources.sh [extra hipcc flags]
 set -e
 cd "$(dirname "$0")/.."
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c --offload-device-only -Iinclude -Ibioimitation-gym_amd/csrc \
+# the shipped library's flags (bioimitation/_buildinfo.py: one place for them)
+FLAGS=$(cd bioimitation-gym_amd && python3 -m bioimitation._buildinfo flags)
+hipcc $FLAGS -c --offload-device-only \
     -Rpass-analysis=kernel-resource-usage "$@" -o /tmp/bioim_res.o bioimitation-gym_amd/csrc/bioim_step.hip 2>&1 |
     python3 -c "
 import re, sys

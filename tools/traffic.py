@@ -4,9 +4,11 @@ bench.py's lookup: '<env_id>/fp<precision>/<envs>'.
 
 Per MI355X_MICROARCH.md (HBM/rocprofv3 section): FETCH_SIZE counts 64 B per
 memory-side read request and reads exactly 1/2 of the bytes of wide (16 B/lane)
-coalesced streams; the env kernel's loads are 8 B/lane SoA rows, an
-uncalibrated width, so the raw value is recorded next to the doubled one and
-bench.py reports the raw FETCH + WRITE sum (a lower bound on bytes moved).
+coalesced streams.  The env kernel's loads are 8 B/lane SoA rows of 16
+consecutive envs (128 B per workgroup row), i.e. whole 128-B requests, so the
+doubled value is the byte count: ``bytes`` = 2 x FETCH_SIZE + WRITE_SIZE
+(the raw counter is kept next to it).  WRITE_SIZE matches the algorithmic
+write bytes to 0.1 %, which supports reading the counters this way.
 The reset dispatch (first, much shorter) is excluded.
 
     python tools/traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <env_id> <precision> <envs>
@@ -31,7 +33,7 @@ def main():
     d = os.path.dirname(os.path.dirname(fcsv))
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles', 'traffic.json')
     db = json.load(open(out)) if os.path.exists(out) else {}
-    db[f'{env_id}/fp{prec}/{n}'] = {'bytes': fetch + write, 'fetch_bytes_raw': fetch, 'fetch_bytes_x2': 2 * fetch,
+    db[f'{env_id}/fp{prec}/{n}'] = {'bytes': 2 * fetch + write, 'fetch_bytes_raw': fetch, 'fetch_bytes_x2': 2 * fetch,
                                     'write_bytes': write, 'source': d}
     json.dump(db, open(out, 'w'), indent=1, sort_keys=True)
     print(json.dumps(db[f'{env_id}/fp{prec}/{n}']))
