@@ -199,6 +199,15 @@ class CoordinateActuator:
 
 
 @dataclass
+class Marker:
+    """MarkerSet station: a point fixed in a body frame (used by OpenSim's
+    InverseKinematicsTool; tests/test_ik_pin.py pins our kinematics with it)."""
+    name: str
+    body: str
+    location: np.ndarray
+
+
+@dataclass
 class OsimModel:
     name: str
     gravity: np.ndarray
@@ -213,6 +222,7 @@ class OsimModel:
     hc_forces: List[HuntCrossley] = field(default_factory=list)
     limits: List[CoordinateLimit] = field(default_factory=list)
     coord_actuators: List[CoordinateActuator] = field(default_factory=list)
+    markers: List[Marker] = field(default_factory=list)
 
     def total_mass(self) -> float:
         return float(sum(b.mass for b in self.bodies.values()))
@@ -463,6 +473,16 @@ def _parse_v4(model_elem) -> OsimModel:
                      joints, coords, corder)
 
 
+def _parse_markers(model_elem, model: OsimModel):
+    """MarkerSet (4.x: socket_parent_frame '/bodyset/<body>'; 3.x: <body>)."""
+    ms = model_elem.find('MarkerSet/objects')
+    if ms is None:
+        return
+    for m in ms.findall('Marker'):
+        frame = m.findtext('socket_parent_frame') or m.findtext('body') or ''
+        model.markers.append(Marker(m.get('name'), frame.strip().split('/')[-1], _vec3(m.findtext('location'))))
+
+
 def load_osim(path: str) -> OsimModel:
     root = _read_xml(path)
     version = int(root.get('Version', '30000'))
@@ -470,6 +490,7 @@ def load_osim(path: str) -> OsimModel:
     model = _parse_v3(me) if version < 40000 else _parse_v4(me)
     _parse_forces(me, model)
     _parse_contact_geometry(me, model)
+    _parse_markers(me, model)
     # PinJoint/WeldJoint coordinate lists follow the SpatialTransform defaults
     for j in model.joints:
         for c in j.coords:

@@ -147,3 +147,52 @@ def test_full_grid_4096_envs_vs_oracle(env_id):
     print(f'{env_id} 4096 envs x {T} steps: {len(check)} envs checked (first/last workgroup included), '
           f'max rel err {worst:.2e}, alive {alive.sum()}/{len(check)}')
     env.close()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+@pytest.mark.parametrize('tag', ['3D', '02905'])
+def test_ik_frames_body_positions_on_hip_path(tag):
+    """Closes the OpenSim-IK pin (tests/test_ik_pin.py) on the HIP path: one
+    env per IK frame, its coordinates set to OpenSim's IK solution, stepped
+    over a zero-length interval (time already at 0.01 * (istep + 1): the same
+    zero-length step the reference takes after the int(t/0.01) truncation,
+    opensim_wrapper.py:299-307), so the reported observation is the kinematics
+    of exactly that state.  Every body position, coordinate and COM column
+    must equal the oracle's, whose forward kinematics the IK frames pin."""
+    import torch
+    import oracle
+    from bioimitation.obslayout import column_names, load_names
+    from bioimitation.registry import load_pack
+    from bioimitation.vector_env import VectorEnv
+    z = np.load(os.path.join(HERE, 'golden', f'ik_{tag}.npz'), allow_pickle=False)
+    env_id = str(z['env_id'])
+    pk = load_pack(env_id)
+    n = len(z['q'])
+    env = VectorEnv(env_id, n, precision=64, seed=1)
+    env.reset(ref_index=np.full(n, 10))
+    st = env.get_state()
+    nd = pk.ndof
+    dof = np.array([pk.coord[c].dof for c in range(pk.ncoord)])
+    k = 40
+    st[:, 0], st[:, 1] = 0.01 * (k + 1), k
+    st[:, 5 + nd:5 + 2 * nd] = 0.0
+    for c in range(pk.ncoord):
+        if dof[c] >= 0:
+            st[:, 5 + dof[c]] = z['q'][:, c]
+    env.set_state(st)
+    acts = np.full((n, pk.nact), 0.1)
+    obs = env.step(torch.as_tensor(acts, device=env.device))[0].cpu().numpy()
+    assert np.abs(env.get_state()[:, 5:5 + nd] - st[:, 5:5 + nd]).max() == 0.0      # zero-length step
+    orc = oracle.Oracle(pk)
+    bufs = orc.new_envs(n)
+    names = column_names(pk, load_names(env_id))
+    cols = [i for i, c in enumerate(names) if c.startswith(('body_pos', 'coordinate_pos'))]
+    assert len(cols) > 30
+    worst = 0.0
+    for i in range(n):
+        orc.set_state(bufs, i, st[i])
+        o = orc.step(bufs, i, acts[i])[0]
+        worst = max(worst, _rel(obs[i, cols], o[cols]).max())
+    print(f'{tag}: {n} IK frames, {len(cols)} body-position / coordinate columns, HIP vs oracle max rel err {worst:.2e}')
+    assert worst < 1e-12
+    env.close()
