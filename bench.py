@@ -138,6 +138,8 @@ def main():
     ap.add_argument('--envs', type=int, default=4096, help='envs per GPU')
     ap.add_argument('--precision', type=int, default=int(os.environ.get('BIOIM_PRECISION', 64)))
     ap.add_argument('--env-id', default='MuscleWalkingImitation2D-v0')
+    ap.add_argument('--integrator', default='semi-implicit', choices=['semi-implicit', 'rk-merson'],
+                    help="'rk-merson': the reference's adaptive integrator at accuracy 1e-3 (DESIGN.md §3)")
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--mixed', default=None,
                     help="mixed batch 'ID_A,ID_B' split 50/50 per GPU (BASELINE config C5), e.g. "
@@ -171,16 +173,16 @@ def main():
         ids = a.mixed.split(',')
         sizes = [a.envs // len(ids)] * len(ids)
         sizes[-1] += a.envs - sum(sizes)
-        env = MixedVectorEnv(list(zip(ids, sizes)), device=local, precision=a.precision, seed=1000, auto_reset=True,
-                             env_offset=rank * a.envs)
+        env = MixedVectorEnv(list(zip(ids, sizes)), config={'integrator': a.integrator}, device=local,
+                             precision=a.precision, seed=1000, auto_reset=True, env_offset=rank * a.envs)
         env.pack, env.nsub, env.lanes_per_env = env.envs[0].pack, env.envs[0].nsub, env.envs[0].lanes_per_env
         env.launch = {e.env_id: e.launch for e in env.envs}
         a.env_id = '+'.join(ids)
         a.no_cpu_baseline = True
         handles = env.envs
     else:
-        env = VectorEnv(a.env_id, a.envs, device=local, precision=a.precision, seed=1000, auto_reset=True,
-                        env_offset=rank * a.envs)        # global env index block (bioimitation/parallel.py)
+        env = VectorEnv(a.env_id, a.envs, config={'integrator': a.integrator}, device=local, precision=a.precision,
+                        seed=1000, auto_reset=True, env_offset=rank * a.envs)   # global env index block (parallel.py)
         handles = [env]
     n, A = a.envs, env.action_dim
     pool = 64      # action batches cycled through (uploaded once; inputs resident in HBM)
@@ -238,7 +240,9 @@ def main():
             'burn_in': a.burn_in, 'ms_per_step': t_max / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': f'f{a.precision}', 'done_rate': done_rate,
             'data': 'synthetic: PCG64 U[0,1] muscle excitations; reference motion synthesized from the shipped 3D IK',
-            'config': {'workload': f'{a.env_id} batched env.step, {n} envs/GPU, nsub={env.nsub}, auto-reset',
+            'config': {'workload': f'{a.env_id} batched env.step, {n} envs/GPU, ' +
+                       (f'nsub={env.nsub}' if a.integrator == 'semi-implicit' else 'RK-Merson 1e-3') + ', auto-reset',
+                       'integrator': a.integrator,
                        'envs_per_gpu': n, 'lanes_per_env': env.lanes_per_env, 'parallelism': f'env-shard x{world}',
                        'launch': env.launch},
             'roofline': roofline,

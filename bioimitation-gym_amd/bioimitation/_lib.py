@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get('BIOIM_LIB', os.path.join(PKG_ROOT, 'build', 'libbioim
 
 EXPORTS = ['bioim_create', 'bioim_destroy', 'bioim_reset', 'bioim_step', 'bioim_set_auto_reset', 'bioim_set_env_offset', 'bioim_set_io_strides', 'bioim_step_group', 'bioim_set_perturbation', 'bioim_id_eval', 'bioim_state_dim',
            'bioim_get_state', 'bioim_set_state', 'bioim_query', 'bioim_query_launch', 'bioim_stream', 'bioim_set_stream', 'bioim_sync',
-           'bioim_last_error', 'bioim_modelpack_size', 'bioim_build_id', 'bioim_reset_count', 'bioim_set_final_obs']
+           'bioim_last_error', 'bioim_modelpack_size', 'bioim_build_id', 'bioim_reset_count', 'bioim_set_final_obs', 'bioim_set_integrator']
 
 _lib = None
 
@@ -58,6 +58,7 @@ def load():
         'bioim_build_id': (C.c_char_p, []),
         'bioim_reset_count': (C.c_int, [vp, C.POINTER(C.c_uint64)]),
         'bioim_set_final_obs': (C.c_int, [vp, vp]),
+        'bioim_set_integrator': (C.c_int, [vp, C.c_int, C.c_double]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

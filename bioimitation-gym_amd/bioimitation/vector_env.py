@@ -25,6 +25,8 @@ import numpy as np
 from . import _lib
 from .registry import load_pack
 
+INTEGRATORS = {'semi-implicit': 0, 'rk-merson': 1}
+
 
 class VectorEnv:
     def __init__(self, env_id: str, num_envs: int, config: dict = None, device: int = 0, precision: int = 64,
@@ -54,6 +56,13 @@ class VectorEnv:
         self.launch = dict(lanes_per_env=ql[0], threads_per_workgroup=ql[1], envs_per_workgroup=ql[2],
                            lds_bytes_per_workgroup=ql[3], workgroups=ql[4])
         _lib.check(L.bioim_set_auto_reset(h, 1 if auto_reset else 0))
+        # config 'integrator': 'semi-implicit' (fixed substeps, the default) or 'rk-merson' (the
+        # reference's adaptive integrator at 'integrator_accuracy', default the env's 1e-3)
+        self.integrator = (config or {}).get('integrator', 'semi-implicit')
+        if self.integrator not in INTEGRATORS:
+            raise ValueError(f"integrator must be one of {sorted(INTEGRATORS)}, got {self.integrator!r}")
+        self.integrator_accuracy = float((config or {}).get('integrator_accuracy', 1e-3))
+        _lib.check(L.bioim_set_integrator(h, INTEGRATORS[self.integrator], self.integrator_accuracy))
         _lib.check(L.bioim_set_env_offset(h, int(env_offset)))
         self.env_offset = int(env_offset)
         n = self.num_envs

@@ -207,4 +207,5 @@ struct DState {
     Real *q, *u, *act, *lce, *hist, *last, *old_px; /* [ndof][N] [ndof][N] [nm][N] [nm][N] [H][nact][N] [nact][N] [N] */
     double *t;
     int32_t *istep, *has_last, *done, *resets;
+    double *hrk;   /* [N] RK-Merson step size carried to the next env step (0: none yet) */
 };

@@ -1790,10 +1790,41 @@ template <class T, typename Real> struct LaunchArgs {
     const double *pert_x;
     const Real *pert_y;
     int pert_n, pert_ob;
+    double rk_acc;     /* RK-Merson accuracy (RK kernels) */
 };
 
-/* One 256-thread workgroup = 256/G envs of segment `a`, block `blk`. */
-template <class T, typename Real, bool PERT>
+/* Reference integrator (RK kernels): OpenSim's Manager integrates with an
+ * adaptive Kutta-Merson 4(5) at accuracy 1e-3 (opensim_wrapper.py:287-301).
+ * Stage form, error norm, step control and the attempt cap follow
+ * oracle/bioim_oracle.c integrate_rk_merson exactly; per state value the lane
+ * keeps y0, K, E (three registers) besides the value itself. */
+#define BIOIM_RK_MAX_ATTEMPTS 4096
+template <typename Real> DEV void rk_update(int s, Real h, Real f, Real &y, Real &y0, Real &K, Real &E, Real &err) {
+    switch (s) {
+    case 0: y0 = y; K = f; E = Real(2) * f; y = y0 + h / Real(3) * f; break;
+    case 1: y = y0 + h / Real(6) * (K + f); break;
+    case 2: E -= Real(9) * f; y = y0 + h / Real(8) * (K + Real(3) * f); break;
+    case 3: {
+        const Real B = (K + E) / Real(3);
+        E += Real(8) * f;
+        y = y0 + Real(0.5) * h * (B + Real(4) * f);
+        K += Real(4) * f;
+        break;
+    }
+    default: {
+        E -= f;
+        y = y0 + h / Real(6) * (K + f);
+        const Real w = fabs(y0) > Real(1) ? fabs(y0) : Real(1);
+        const Real ei = fabs(h / Real(30) * E) / w;
+        if (!(ei <= err)) err = ei;
+    }
+    }
+}
+
+/* One 256-thread workgroup = 256/G envs of segment `a`, block `blk`.
+ * RK: the reference integrator (adaptive Kutta-Merson) instead of the
+ * fixed semi-implicit substeps. */
+template <class T, typename Real, bool PERT, bool RK>
 DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     using LY = Lay<T, Real>;
     constexpr int G = T::G, ND = LY::ND, NA = T::NA, NM = T::NM;
@@ -1869,6 +1900,14 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
 
     int remaining = 0;
     Real dt = 0;
+    /* RK kernels: current step [rk_t, rk_t + rk_h], stage, attempts, next step size */
+    double rk_t = 0, rk_tf = 0, rk_h = 0, rk_hnext = RK ? st.hrk[env] : 0.0;
+    int rk_stage = 0, rk_attempts = 0;
+    bool rk_last = false, rk_fail = false;
+    Real y0q = 0, y0u = 0, Kq = 0, Ku = 0, Eq = 0, Eu = 0, rk_err = 0;
+    Real y0a[MPL], y0l[MPL], Ka[MPL], Kl[MPL], Ea[MPL], El[MPL];
+#pragma unroll
+    for (int j = 0; j < MPL; ++j) { y0a[j] = y0l[j] = Ka[j] = Kl[j] = Ea[j] = El[j] = 0; }
     const PertArgs<Real> PA{a.pert_x, a.pert_y, a.pert_n, a.pert_ob, env, N};
     double *pslot = reinterpret_cast<double *>(smem_raw + SMB + sizeof(Real) * EPB * LY::SIZE) + PERT_SLOT * slot;
     if (PERT && lane == 0) { pslot[0] = t; pslot[1] = 0; pslot[2] = 0; pslot[3] = -1; pslot[4] = 0; }
@@ -1950,10 +1989,16 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         double tf = M.step_size * (double)istep;
         double hstep = tf - t;
         if (hstep > 0) {
-            dt = Real(hstep / (double)M.nsub);
-            remaining = M.nsub;
-            /* substep k starts at t + k * hstep / nsub (the oracle's substep times) */
-            if (PERT && lane == 0) { pslot[0] = t; pslot[1] = hstep / (double)M.nsub; }
+            if constexpr (RK) {
+                rk_t = t; rk_tf = tf;
+                rk_h = rk_hnext > 0 ? rk_hnext : 1e-4;
+                remaining = 1;      /* integrating until rk_t reaches rk_tf */
+            } else {
+                dt = Real(hstep / (double)M.nsub);
+                remaining = M.nsub;
+                /* substep k starts at t + k * hstep / nsub (the oracle's substep times) */
+                if (PERT && lane == 0) { pslot[0] = t; pslot[1] = hstep / (double)M.nsub; }
+            }
         }
         t = tf;
     }
@@ -1963,6 +2008,17 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
      * reference row and folds the muscle fiber equilibrium into its realize. */
     bool pending_reset = (mode == 1), reported_reset = false;
     for (;;) {
+        if constexpr (RK) {
+            if (remaining > 0 && rk_stage == 0) {   /* start an RK step, or stop */
+                if (!(rk_tf - rk_t > 1e-14 * (1.0 + fabs(rk_tf)))) remaining = 0;
+                else if (++rk_attempts > BIOIM_RK_MAX_ATTEMPTS) { rk_fail = true; remaining = 0; }
+                else {
+                    rk_last = false;
+                    if (rk_h >= rk_tf - rk_t) { rk_h = rk_tf - rk_t; rk_last = true; }
+                    rk_err = 0;
+                }
+            }
+        }
         const bool sub = remaining > 0;
         const bool eq = !sub && pending_reset;
         if (eq) {
@@ -1975,6 +2031,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             t = M.ref_time[r];
             istep = M.ref_istep[r];
             has_last = 0;
+            rk_hnext = 0;   /* reset_manager: a new integrator (opensim_wrapper.py:287-291) */
 #pragma unroll
             for (int j = 0; j < MPL; ++j) control[j] = 0;
             resets += 1;
@@ -1988,10 +2045,63 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             asm volatile("" : "+s"(Mi));
             /* realize / reset realize: the call time is t itself */
             if (PERT && !sub && lane == 0) { pslot[0] = t; pslot[1] = 0; }
-            dynamics<T, Real, PERT>(*(const DModel<Real> *)Mi, SM, qd, ud, act, lce, control, lane, lds, sub ? dt : Real(0),
-                              eq && NM > 0, PA, pslot, M.nsub - remaining, D);
+            if (RK && PERT && sub && lane == 0) {
+                const double cs = rk_stage == 0 ? 0.0 : rk_stage <= 2 ? 1.0 / 3.0 : rk_stage == 3 ? 0.5 : 1.0;
+                pslot[0] = rk_t + cs * rk_h; pslot[1] = 0;
+            }
+            /* RK: explicit accelerations (h = 0, the implicit terms compile away) */
+            dynamics<T, Real, PERT>(*(const DModel<Real> *)Mi, SM, qd, ud, act, lce, control, lane, lds,
+                                    RK ? Real(0) : (sub ? dt : Real(0)), eq && NM > 0, PA, pslot,
+                                    RK ? 0 : M.nsub - remaining, D);
         }
-        if (sub) {
+        if (RK && sub) {
+            const Real h = Real(rk_h);
+            if (lane < ND) {
+                const Real fq = ud, fu = D.qdd;
+                rk_update<Real>(rk_stage, h, fq, qd, y0q, Kq, Eq, rk_err);
+                rk_update<Real>(rk_stage, h, fu, ud, y0u, Ku, Eu, rk_err);
+            }
+            if constexpr (NM > 0) {
+#pragma unroll
+                for (int j = 0; j < MPL; ++j) {
+                    const int m = mslot<T>(lane + j * G);
+                    if (m < NM) {
+                        const Real fl = D.ms[j].clamped ? Real(0) : D.ms[j].vce;
+                        rk_update<Real>(rk_stage, h, D.ms[j].dadt, act[j], y0a[j], Ka[j], Ea[j], rk_err);
+                        rk_update<Real>(rk_stage, h, fl, lce[j], y0l[j], Kl[j], El[j], rk_err);
+                    }
+                }
+            }
+            if (rk_stage < 4) {
+                ++rk_stage;
+                continue;
+            }
+            rk_stage = 0;
+            Real e = isnan(rk_err) ? Real(INFINITY) : rk_err;
+            e = group_max<G>(e);
+            const double err = (double)e;
+            double fac = err > 0 ? 0.9 * sqrt(sqrt(a.rk_acc / err)) : 5.0;
+            if (!(fac == fac)) fac = 0.1;
+            fac = fac < 0.1 ? 0.1 : (fac > 5.0 ? 5.0 : fac);
+            if (err <= a.rk_acc) {
+                if constexpr (NM > 0) {
+#pragma unroll
+                    for (int j = 0; j < MPL; ++j) {
+                        const int m = mslot<T>(lane + j * G);
+                        if (m < NM && lce[j] < SM.mus[m].lmin) lce[j] = SM.mus[m].lmin;
+                    }
+                }
+                rk_t = rk_last ? rk_tf : rk_t + rk_h;
+                if (!rk_last) rk_hnext = rk_h * fac;
+            } else {
+                qd = y0q; ud = y0u;
+#pragma unroll
+                for (int j = 0; j < MPL; ++j) { act[j] = y0a[j]; lce[j] = y0l[j]; }
+            }
+            rk_h *= fac;
+            continue;
+        }
+        if (!RK && sub) {
             if (lane < ND) { ud += dt * D.qdd; qd += dt * ud; }
             if constexpr (NM > 0) {
 #pragma unroll
@@ -2196,7 +2306,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                 if (lds[LY::REP + 6 * T::CALCN_R + 2] - lds[LY::REP + 6 * T::CALCN_L + 2] < 0) d_ = 1;
             }
             if (group_any<G>(lane < ND && (!isfinite(qd) || !isfinite(ud)))) d_ = 1;
-            if (!D.ok) d_ = 1;
+            if (!D.ok || rk_fail) d_ = 1;
             done = d_;
         }
         if (lane == 0) {
@@ -2230,6 +2340,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         st.old_px[env] = old_px;
         st.done[env] = (mode == 0 && !do_reset) ? done : 0;
         st.resets[env] = resets;
+        if (RK || mode == 1) st.hrk[env] = rk_hnext;
     }
     if (lane < ND) {
         st.q[(size_t)lane * N + env] = qd;
@@ -2245,9 +2356,9 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     }
 }
 
-template <class T, typename Real, bool PERT>
+template <class T, typename Real, bool PERT, bool RK>
 __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))) void env_kernel(LaunchArgs<T, Real> a) {
-    env_block<T, Real, PERT>(a, blockIdx.x);
+    env_block<T, Real, PERT, RK>(a, blockIdx.x);
 }
 
 
@@ -2648,6 +2759,8 @@ struct bioim_handle {
     void *pert_x, *pert_y; /* apply_perturbations table: double [pert_n], Real [pert_n][n] */
     int pert_n, pert_ob;
     void *final_obs;    /* caller's device buffer [n][obs_stride] or null (bioim_set_final_obs) */
+    int rk;             /* integrator: 0 semi-implicit substeps (pack nsub), 1 RK-Merson (bioim_set_integrator) */
+    double rk_acc;
     Ops ops;
     bioim_modelpack_t pack;
 };
@@ -2682,6 +2795,7 @@ LaunchArgs<T, Real> make_args(bioim_handle_t *h, int mode, const void *actions, 
     a.pert_x = reinterpret_cast<const double *>(h->pert_x);
     a.pert_y = reinterpret_cast<const Real *>(h->pert_y);
     a.pert_n = h->pert_n; a.pert_ob = h->pert_ob;
+    a.rk_acc = h->rk_acc;
     return a;
 }
 
@@ -2692,13 +2806,12 @@ void launch_impl(bioim_handle_t *h, int mode, const void *actions, void *obs, vo
     if (a.blocks <= 0) return;
     /* the perturbation kernels are separate instantiations, so the default
      * kernels' code is untouched by the (rarely used) push */
-    if (a.pert_n > 0) {
-        constexpr size_t lds = lds_bytes<T, Real, true>();
-        hipLaunchKernelGGL((env_kernel<T, Real, true>), dim3(a.blocks), dim3(BIOIM_WG), lds, h->stream, a);
-    } else {
-        constexpr size_t lds = lds_bytes<T, Real, false>();
-        hipLaunchKernelGGL((env_kernel<T, Real, false>), dim3(a.blocks), dim3(BIOIM_WG), lds, h->stream, a);
-    }
+    constexpr size_t lds0 = lds_bytes<T, Real, false>(), lds1 = lds_bytes<T, Real, true>();
+    const dim3 g(a.blocks), b(BIOIM_WG);
+    if (a.pert_n > 0 && h->rk) hipLaunchKernelGGL((env_kernel<T, Real, true, true>), g, b, lds1, h->stream, a);
+    else if (a.pert_n > 0) hipLaunchKernelGGL((env_kernel<T, Real, true, false>), g, b, lds1, h->stream, a);
+    else if (h->rk) hipLaunchKernelGGL((env_kernel<T, Real, false, true>), g, b, lds0, h->stream, a);
+    else hipLaunchKernelGGL((env_kernel<T, Real, false, false>), g, b, lds0, h->stream, a);
 }
 
 template <class T, typename Real>
@@ -2716,9 +2829,13 @@ void id_launch_impl(bioim_handle_t *h, int op, int n, const void *q, const void 
 
 template <class T, typename Real> int upload_smodel(bioim_handle_t *h) {
     static_assert(lds_bytes<T, Real, true>() <= 163840, "LDS image + env regions exceed 160 KiB");
-    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, false>),
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, false, false>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, false>()));
-    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, true>),
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, true, false>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, true>()));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, false, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, false>()));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, true, true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, true>()));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&id_kernel<T, Real>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, false>()));
@@ -2761,12 +2878,13 @@ template <typename Real> size_t state_layout(bioim_handle_t *h, char *base, DSta
     size_t oh = take(sizeof(Real) * BIOIM_MAX_HORIZON * h->nact * n), olast = take(sizeof(Real) * h->nact * n);
     size_t opx = take(sizeof(Real) * n), ot = take(sizeof(double) * n);
     size_t oi = take(sizeof(int32_t) * n), ohl = take(sizeof(int32_t) * n), od = take(sizeof(int32_t) * n),
-           orr = take(sizeof(int32_t) * n);
+           orr = take(sizeof(int32_t) * n), ohr = take(sizeof(double) * n);
     if (st) {
         st->q = (Real *)(base + oq); st->u = (Real *)(base + ou); st->act = (Real *)(base + oa);
         st->lce = (Real *)(base + ol); st->hist = (Real *)(base + oh); st->last = (Real *)(base + olast);
         st->old_px = (Real *)(base + opx); st->t = (double *)(base + ot); st->istep = (int32_t *)(base + oi);
         st->has_last = (int32_t *)(base + ohl); st->done = (int32_t *)(base + od); st->resets = (int32_t *)(base + orr);
+        st->hrk = (double *)(base + ohr);
     }
     return off;
 }
@@ -2811,6 +2929,7 @@ template <typename Real> int xfer_state(bioim_handle_t *h, double *host, const d
             for (int hh = 0; hh < H; ++hh)
                 for (int i = 0; i < na; ++i) s[k++] = hs.hist[(hh * na + i) * n + e];
             for (int i = 0; i < na; ++i) s[k++] = hs.last[i * n + e];
+            s[k++] = hs.hrk[e];
         } else {
             const double *s = in + e * dim;
             int k = 0;
@@ -2823,6 +2942,7 @@ template <typename Real> int xfer_state(bioim_handle_t *h, double *host, const d
             for (int hh = 0; hh < H; ++hh)
                 for (int i = 0; i < na; ++i) hs.hist[(hh * na + i) * n + e] = (Real)s[k++];
             for (int i = 0; i < na; ++i) hs.last[i * n + e] = (Real)s[k++];
+            hs.hrk[e] = s[k++];
         }
     }
     if (in) HIPCHK(hipMemcpy(h->state_buf, buf.data(), h->state_bytes, hipMemcpyHostToDevice));
@@ -2952,6 +3072,14 @@ int bioim_set_auto_reset(bioim_handle_t *h, int on) {
     return 0;
 }
 
+int bioim_set_integrator(bioim_handle_t *h, int kind, double accuracy) {
+    if (!h || kind < 0 || kind > 1 || (kind == 1 && !(accuracy > 0)))
+        return fail(BIOIM_E_ARG, "bioim_set_integrator: kind 0 (semi-implicit) or 1 (RK-Merson, accuracy > 0)");
+    h->rk = kind;
+    h->rk_acc = kind == 1 ? accuracy : 0.0;
+    return 0;
+}
+
 int bioim_set_final_obs(bioim_handle_t *h, void *final_obs) {
     if (!h) return fail(BIOIM_E_ARG, "null handle");
     h->final_obs = final_obs;
@@ -3059,7 +3187,7 @@ int bioim_set_env_offset(bioim_handle_t *h, int offset) {
 
 int bioim_state_dim(const bioim_handle_t *h) {
     if (!h) return fail(BIOIM_E_ARG, "null handle");
-    return 5 + 2 * h->ndof + 2 * h->nmuscle + h->horizon * h->nact + h->nact;
+    return 5 + 2 * h->ndof + 2 * h->nmuscle + h->horizon * h->nact + h->nact + 1;
 }
 
 int bioim_get_state(bioim_handle_t *h, double *host_state) {

@@ -137,6 +137,14 @@ int bioim_state_dim(const bioim_handle_t *h);
 int bioim_get_state(bioim_handle_t *h, double *host_state /* [N][state_dim] */);
 int bioim_set_state(bioim_handle_t *h, const double *host_state);
 
+/* Integrator of the physics between env steps.  kind 0: the fixed
+ * semi-implicit substeps (the pack's nsub; default).  kind 1: the reference's
+ * integrator, an adaptive Kutta-Merson 4(5) at `accuracy` (OpenSim's
+ * Manager, opensim_wrapper.py:287-301, accuracy 1e-3 from
+ * muscle_walking_imitation_env2D.py:42), restated in
+ * oracle/bioim_oracle.c integrate_rk_merson.  Replaces the integrator
+ * choice inside OsimModel.reset_manager. */
+int bioim_set_integrator(bioim_handle_t *h, int kind, double accuracy);
 /* Optional terminal-observation output: when set (a device buffer with the
  * handle's obs row stride), every step also writes each env's observation
  * as computed by that step *before* an in-kernel auto-reset replaces it, so

@@ -50,6 +50,8 @@ class Oracle:
             ('orc_contact', None, [C.c_void_p, _dp, _dp, _dp, _dp]),
             ('orc_batch_step', C.c_int, [C.c_void_p, C.c_int, C.c_void_p, _dp, _dp, _dp,
                                          C.POINTER(C.c_int32), _dp, C.c_int]),
+            ('orc_env_set_integrator', C.c_int, [C.c_void_p, C.c_int, C.c_double]),
+            ('orc_env_rk_stats', None, [C.c_void_p, _dp]),
         ]:
             f = getattr(L, name)
             f.restype = res
@@ -92,6 +94,19 @@ class Oracle:
         rc = self.lib.orc_env_set_perturbation(self.pk, self.env_ptr(envs, i), int(os_body), len(x), _ptr(x), _ptr(y))
         if rc:
             raise ValueError('orc_env_set_perturbation: bad table')
+
+    def set_integrator(self, envs, i, kind, accuracy=1e-3):
+        """kind 'euler' (the kernel's fixed-substep semi-implicit scheme) or
+        'rk-merson' (the reference's adaptive integrator at `accuracy`)."""
+        k = {'euler': 0, 'rk-merson': 1, 'extrap2': 2, 'extrap3': 3, 'extrap-adaptive': 4}[kind]
+        if self.lib.orc_env_set_integrator(self.env_ptr(envs, i), k, float(accuracy)):
+            raise ValueError('orc_env_set_integrator: bad arguments')
+
+    def rk_stats(self, envs, i):
+        """(accepted steps, rejected steps, smallest step, next step) since set_integrator"""
+        out = np.zeros(4)
+        self.lib.orc_env_rk_stats(self.env_ptr(envs, i), _ptr(out))
+        return out
 
     def state_dim(self):
         return self.lib.orc_state_dim(self.pk)

@@ -453,3 +453,63 @@ def test_parity_200_steps_through_termination(env_id):
           f'{worst[0]:.1e}/{worst[49]:.1e}/{worst[99]:.1e}/{worst[-1]:.1e}; {ever_done.sum()}/{n} envs terminated')
     assert worst.max() < 1e-4, (int(worst.argmax()), worst.max())
     env.close()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+@pytest.mark.parametrize('env_id', ['MuscleWalkingImitation2D-v0', 'TorqueWalkingImitation2D-v0',
+                                    'MuscleRunningImitation3D-v0', 'MuscleLockedKneeImitation3D-v0',
+                                    'MusclePalsyImitation3D-v0', 'TorqueWalkingImitation3D-v0',
+                                    'TorqueLockedKneeImitation2D-v0'])
+def test_rk_merson_parity_fp64(env_id):
+    """config integrator='rk-merson' (the reference's adaptive Kutta-Merson at
+    accuracy 1e-3, opensim_wrapper.py:287-301) on the GPU vs the oracle's
+    integrate_rk_merson (same stage form, error norm and step control).
+    Each step starts from the oracle's state (re-synced, state includes the
+    carried step size), because adaptive stepping is not bitwise-stable:
+    the step size is a continuous function of the error estimate, whose
+    inputs include q'' — near contact the accelerations move by ~1e-5
+    relative for 1e-12 m of state, so the GPU's and the oracle's step
+    sequences drift apart by ~1e-9..1e-6 relative and an accept/reject test
+    can land on either side.  Bounds per step: observation columns other
+    than q'' and the next state within 1e-4 relative (north_star), >= 95 % of
+    env steps within 1e-8; q'' (coordinate_acc) within 1e-2 of max(|q''|, 1)."""
+    import torch
+    rng = np.random.default_rng(12)
+    n, T = 40, 30
+    cfg = {'integrator': 'rk-merson'}
+    rows = np.concatenate([QUIRK_ROWS, rng.integers(0, 120, size=n - len(QUIRK_ROWS))])
+    pk, env, orc, bufs = _setup(env_id, n, 64, config=cfg)
+    for i in range(n):
+        orc.set_integrator(bufs, i, 'rk-merson', 1e-3)
+    env.reset(ref_index=rows)
+    for i in range(n):
+        orc.reset(bufs, i, int(rows[i]))
+    qdd = _qdd_cols(pk)
+    other = np.setdiff1d(np.arange(env.obs_dim), qdd)
+    errs, qerr, serr = [], 0.0, 0.0
+    for t in range(T):
+        env.set_state(np.stack([orc.get_state(bufs, i) for i in range(n)]))
+        st = np.array([orc.get_state(bufs, i)[1] for i in range(n)]).astype(int)
+        acts = _actions(env_id, rng, n, env.action_dim, pk, st + 1)
+        if 'Muscle' in env_id:
+            acts *= 0.5
+        obs, rew, done, info = env.step(torch.as_tensor(acts, device=env.device))
+        torch.cuda.synchronize()
+        obs, rew, done, info = (x.cpu().numpy() for x in (obs, rew, done, info))
+        gst = env.get_state()
+        for i in range(n):
+            o, r, d, inf = orc.step(bufs, i, acts[i])
+            e = max(_rel(obs[i], o)[other].max(), abs(rew[i] - r), _rel(info[i], inf).max())
+            errs.append(e)
+            qerr = max(qerr, _rel(obs[i], o)[qdd].max())
+            s = orc.get_state(bufs, i)
+            serr = max(serr, _rel(gst[i, 5:-1], s[5:-1]).max())
+            assert bool(done[i]) == d or e > 1e-8, (t, i)
+            if d:
+                orc.reset(bufs, i, int(rng.integers(0, 120)))
+    errs = np.array(errs)
+    frac = float((errs <= 1e-8).mean())
+    print(f'{env_id} RK-Merson fp64, {len(errs)} re-synced env steps: obs/reward max rel err {errs.max():.2e}, '
+          f'{100 * frac:.1f} % <= 1e-8, median {np.median(errs):.1e}; q\'\' {qerr:.1e}; state {serr:.1e}')
+    assert errs.max() < 1e-4 and serr < 1e-4 and frac >= 0.95 and qerr < 1e-2
+    env.close()

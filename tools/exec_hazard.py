@@ -1,0 +1,116 @@
+"""Scan gfx950 assembly for register copies executed under a narrowed EXEC
+that move a value defined before the divergent region into a register read
+after the region joins (the wrong-lane / fault incidents).
+
+A structured `if` in the ISA is
+    s_and_saveexec_b64 s[a:b], vcc     ; EXEC narrowed to the taken lanes
+    ...                                 ; region
+    s_or_b64 exec, exec, s[a:b]        ; join: EXEC restored
+A VGPR <-> AGPR copy (v_accvgpr_write / v_accvgpr_read / v_mov_b32) inside
+the region writes only the active lanes.  If its source was defined before
+the region (the value is live in every lane) and its destination is read
+after the join before being rewritten, the inactive lanes read whatever the
+destination held before: a value silently lost in those lanes.  The scan is
+linear over each kernel (loop back-edges are ignored), so it reports
+candidates; each must be checked by hand.
+
+    python tools/exec_hazard.py <file.s> [kernel-substring]
+"""
+import re
+import sys
+
+REG = re.compile(r'\b([va])(\d+)\b|\b([va])\[(\d+):(\d+)\]')
+
+
+def regs(text):
+    out = []
+    for m in REG.finditer(text):
+        if m.group(1):
+            out.append(f'{m.group(1)}{m.group(2)}')
+        else:
+            out += [f'{m.group(3)}{i}' for i in range(int(m.group(4)), int(m.group(5)) + 1)]
+    return out
+
+
+def parse(lines):
+    """[(op, dst regs, src regs, raw)] for the instructions of one kernel."""
+    ins = []
+    for ln in lines:
+        t = ln.split(';')[0].strip()
+        if not t or t.startswith('.') or t.endswith(':'):
+            continue
+        parts = t.split(None, 1)
+        op = parts[0]
+        args = parts[1] if len(parts) > 1 else ''
+        a = [x.strip() for x in args.split(',')] if args else []
+        stores = op.startswith(('global_store', 'buffer_store', 'ds_write', 'scratch_store', 'flat_store', 's_'))
+        dst = [] if stores or not a else regs(a[0])
+        src = regs(','.join(a if stores else a[1:]))
+        ins.append((op, dst, src, t))
+    return ins
+
+
+def scan(ins):
+    hits = []
+    stack = []   # open regions: (saved-exec sgpr text, start index)
+    for i, (op, dst, src, raw) in enumerate(ins):
+        if op in ('s_and_saveexec_b64', 's_or_saveexec_b64', 's_andn2_saveexec_b64'):
+            stack.append((raw.split(None, 1)[1].split(',')[0].strip(), i))
+            continue
+        if op == 's_or_b64' and raw.split(None, 1)[1].startswith('exec, exec,'):
+            sv = raw.split(',')[-1].strip()
+            while stack:
+                s, _ = stack.pop()
+                if s == sv:
+                    break
+            continue
+        if not stack or op not in ('v_accvgpr_write_b32', 'v_accvgpr_read_b32', 'v_mov_b32', 'v_mov_b64'):
+            continue
+        if not dst or not src:
+            continue
+        start = stack[0][1]
+        # source defined before the outermost open region (not written inside it before i)
+        if any(s in d for j in range(start, i) for d in [ins[j][1]] for s in src):
+            continue
+        # destination read after the region closes (first later access is a read)
+        depth = len(stack)
+        j, d = i + 1, depth
+        closed = False
+        verdict = None
+        while j < len(ins) and verdict is None:
+            o, dd, ss, rr = ins[j]
+            if o in ('s_and_saveexec_b64', 's_or_saveexec_b64', 's_andn2_saveexec_b64'):
+                d += 1
+            elif o == 's_or_b64' and rr.split(None, 1)[1].startswith('exec, exec,'):
+                d -= 1
+                if d < depth:
+                    closed = True
+            if any(x in ss for x in dst):
+                verdict = 'read-after-join' if closed else 'read-inside'
+            elif any(x in dd for x in dst):
+                verdict = 'overwritten'
+            j += 1
+        if verdict == 'read-after-join':
+            hits.append((i, raw, j - 1, ins[j - 1][3]))
+    return hits
+
+
+def main():
+    path = sys.argv[1]
+    want = sys.argv[2] if len(sys.argv) > 2 else ''
+    text = open(path).read().split('\n')
+    starts = [i for i, l in enumerate(text) if re.match(r'^_Z\S+:', l)]
+    for k, s in enumerate(starts):
+        name = text[s].split(':')[0]
+        if want not in name:
+            continue
+        e = next(i for i in range(s, len(text)) if text[i].startswith('.Lfunc_end'))
+        ins = parse(text[s:e])
+        hits = scan(ins)
+        print(f'{name[:90]}: {len(ins)} instructions, {len(hits)} candidate copies')
+        for i, raw, j, use in hits[:12]:
+            print(f'    [{i}] {raw:50s} -> read after join at [{j}] {use}')
+
+
+if __name__ == '__main__':
+    main()
