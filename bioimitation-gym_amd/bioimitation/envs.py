@@ -109,6 +109,8 @@ class ImitationEnv:
         from .simulation_io import OsimModelFacade
         self.osim_model = OsimModelFacade(self._env, load_names(self.env_id), lo, hi)
         self._record = bool(cfg.get('record_trajectory', True))
+        if self._record:
+            self._env.enable_force_report()
         ntrans = sum(1 for c in (pk.coord_tx, pk.coord_ty, pk.coord_tz) if c >= 0)
         self._qdd = slice(1 + (pk.ncoord - ntrans) + pk.ncoord, 1 + (pk.ncoord - ntrans) + 2 * pk.ncoord)
 
@@ -124,7 +126,8 @@ class ImitationEnv:
 
     def _record_row(self, obs):
         if self._record:
-            self.osim_model.recorder.record(self._env.get_state()[0], obs[0, self._qdd].double().cpu().numpy())
+            fr = self._env.force_report[0].double().cpu().numpy()
+            self.osim_model.recorder.record(self._env.get_state()[0], obs[0, self._qdd].double().cpu().numpy(), fr)
 
     def reset(self, obs_as_dict=False):
         index = 0 if self.test else random.randint(0, self._env.pack.reset_hi)

@@ -11,10 +11,15 @@ at every reset (``reset_manager``, :287-291).  So the files hold the
 trajectory since the last reset.
 
 Here the single-env API records the realized state after the reset and after
-every step.  Differences from the reference:
+every step, with the kernel's per-force-element report
+(``bioim_set_force_report``).  Differences from the reference:
 - One row per env step (0.01 s), not per internal RK-Merson step.
-- No ForceReporter file: the HIP step does not export per-force-element
-  values.
+- ForceReporter columns: each muscle / coordinate actuator (its actuation),
+  each Hunt-Crossley force's record values on the ground platform
+  (``<force>.ground.force.X..Z``, ``.torque.X..Z``: the six values the
+  reference itself reads and negates, opensim_wrapper.py:211-219), each
+  CoordinateLimitForce (its generalized force).  The contact record's
+  foot-side entries are not written (their layout is not pinned here).
 
 Column names follow OpenSim 4.1:
 - states: ``/jointset/<joint>/<coord>/value``, ``/speed``,
@@ -47,10 +52,14 @@ class TrajectoryRecorder:
 
     def clear(self):
         self.rows = []
+        self.force_rows = []
 
-    def record(self, state_row: np.ndarray, qdd: np.ndarray):
+    def record(self, state_row: np.ndarray, qdd: np.ndarray, forces: np.ndarray = None):
         """state_row: one env's flat state (include/bioim.h layout);
-        qdd: its observation's coordinate_acc block (all coordinates)."""
+        qdd: its observation's coordinate_acc block (all coordinates);
+        forces: its bioim_set_force_report row."""
+        if forces is not None:
+            self.force_rows.append(np.concatenate([[float(state_row[0])], np.asarray(forces, dtype=np.float64)]))
         pk = self.pack
         nd, nm = pk.ndof, pk.nmuscle
         t = float(state_row[0])
@@ -98,7 +107,26 @@ class TrajectoryRecorder:
             paths[key] = os.path.join(base_dir, f'{prefix}_Kinematics_{key}.sto')
             write_sto(paths[key], ['time'] + coords, np.hstack([t, arr * scale]), name=f'Kinematics_{key}',
                       in_degrees=True)
+        # ForceReporter analysis (printResults, :338)
+        if self.force_rows:
+            pk = self.pack
+            labels = ['time'] + (muscles if pk.nmuscle else list(self.names.get('actuators') or
+                                                                  [f'{c}_actuator' for c in self._act_coords()]))
+            fr = np.array(self.force_rows)
+            cols = [fr[:, :1 + pk.nact]]
+            for i, cf in enumerate(self.names['cforces']):
+                labels += [f'{cf}.ground.{k}.{x}' for k in ('force', 'torque') for x in 'XYZ']
+                cols.append(-fr[:, 1 + pk.nact + 6 * i:1 + pk.nact + 6 * i + 6])    # ground side = -(feet side)
+            o = 1 + pk.nact + 6 * pk.ncforce
+            labels += list(self.names['limits'])
+            cols.append(fr[:, o:o + pk.nlimit])
+            paths['forces'] = os.path.join(base_dir, f'{prefix}_ForceReporter_forces.sto')
+            write_sto(paths['forces'], labels, np.hstack(cols), name='ForceReporter_forces')
         return paths
+
+    def _act_coords(self):
+        coords = list(self.names['coords'])
+        return [coords[self.pack.coordact[a].coord] for a in range(self.pack.nact)]
 
 
 class OsimModelFacade:
@@ -127,5 +155,6 @@ class OsimModelFacade:
         return len(self.action_min)
 
     def save_simulation(self, base_dir):
-        """Writes simulation_States.sto and simulation_Kinematics_{q,u,dudt}.sto."""
+        """Writes simulation_States.sto, simulation_Kinematics_{q,u,dudt}.sto and
+        simulation_ForceReporter_forces.sto."""
         return self.recorder.write(base_dir)

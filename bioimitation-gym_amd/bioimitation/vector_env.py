@@ -117,6 +117,17 @@ class VectorEnv:
             self.final_obs = None
         _lib.check(self._L.bioim_set_final_obs(self._h, self._ptr(self.final_obs)))
 
+    def enable_force_report(self, on: bool = True):
+        """Per-force-element values of every realized state in
+        ``self.force_report`` (N, F), F = bioim_force_report_dim (include/bioim.h)."""
+        import torch
+        if on and getattr(self, 'force_report', None) is None:
+            f = _lib.check(self._L.bioim_force_report_dim(self._h))
+            self.force_report = torch.zeros((self.num_envs, f), dtype=self.dtype, device=self.device)
+        elif not on:
+            self.force_report = None
+        _lib.check(self._L.bioim_set_force_report(self._h, self._ptr(self.force_report)))
+
     @staticmethod
     def _ptr(t):
         return C.c_void_p(t.data_ptr()) if t is not None else None

@@ -46,10 +46,21 @@ struct DCurve {
  * staged into LDS at kernel start, so these lookups are ds_reads (~50 cycles)
  * instead of lane-divergent global loads (~200+ cycles at one wave per SIMD).
  * Curves are deduplicated (all muscles of the shipped models share one set). */
+/* LDS bank padding of the lane-indexed model structs (lane l reads element
+ * m(l) of an array of them): a stride of 50 dwords (fp64: 64-bit reads hit
+ * bank (a/4) mod 64, lanes 0..15 on 16 distinct bank pairs) or 33 dwords
+ * (fp32: 32-bit reads, bank (a/4) mod 32, an odd stride is conflict-free);
+ * unpadded, SMuscle is 48 / 32 dwords: 4-way / 16-way conflicts. */
+#ifndef BIOIM_LDS_PAD
+#define BIOIM_LDS_PAD 1
+#endif
 template <typename Real>
 struct SMuscle {
     Real fiso, lopt, inv_lopt, lts, inv_lts, lv; /* lv = lopt * vmax */
     Real tau_act, tau_deact, amin, beta, width, lmin, slow, mass, default_act, pad;
+#if BIOIM_LDS_PAD
+    Real pad_bank;    /* 17 reals + 16 ints: 50 dwords (fp64), 33 (fp32) */
+#endif
     int32_t pt_off, npt;
     int32_t cv[4]; /* curve indices: fal, fv, fpe, fse */
     /* non-root dofs the path can move (union of its points' dofmasks minus
@@ -66,6 +77,9 @@ struct DPathPt {
     uint32_t dofmask;                         /* dofs moving this point                   */
     int32_t mf[3];                            /* moving point: slot of each axis' function (-1: loc) */
     int32_t pad;
+#if BIOIM_LDS_PAD
+    int32_t pad_bank[2];                      /* 12 ints + 17 reals: 46 dwords (fp64), 29 (fp32) */
+#endif
     Real loc[3], R[9], p[3];
     Real lo, hi;
 };

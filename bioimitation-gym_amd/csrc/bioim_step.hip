@@ -1782,6 +1782,8 @@ template <class T, typename Real> struct LaunchArgs {
     const Real *actions;
     Real *obs, *reward, *info;
     Real *final_obs;   /* optional: the step's observation before any auto-reset (row stride obs_stride) */
+    Real *force_out;   /* optional: per-force-element values of the realized state, row stride force_dim */
+    int force_dim;
     uint8_t *done_out;
     const int32_t *env_ids, *ref_index;
     uint64_t seed;
@@ -2199,6 +2201,35 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             const int og = omus + 3 * NM + 6 * lane;
 #pragma unroll
             for (int i = 0; i < 3; ++i) { ob[og + i] = F[i] / M.weight; ob[og + 3 + i] = Mo[i] / M.moment; }
+        }
+        if (a.force_out) {
+            /* ForceReporter values (opensim_wrapper.py:10-15): actuation of each
+             * muscle (tendon force) or coordinate actuator, the wrench on the feet
+             * of each contact force about the ground origin, each limit force */
+            Real *fo = a.force_out + (size_t)env * a.force_dim;
+#pragma unroll
+            for (int j = 0; j < MPL; ++j) {
+                const int m = mslot<T>(lane + j * G);
+                if (m < NA) {
+                    if constexpr (NM > 0) fo[m] = D.ms[j].Ft;
+                    else fo[m] = control[j] * SM.ca_opt[m];
+                }
+            }
+            if (lane < T::NF) {
+                Real F[3] = {0, 0, 0}, Mo[3] = {0, 0, 0};
+#pragma unroll
+                for (int s2 = 0; s2 < T::NS; ++s2) {
+                    const Real *cw = lds + LY::CW + 8 * s2;
+                    const bool mine = SM.sph_force[s2] == lane;
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) { F[i] += mine ? cw[i] : Real(0); Mo[i] += mine ? cw[3 + i] : Real(0); }
+                }
+                Mo[1] += -x0 * F[2];
+                Mo[2] += x0 * F[1];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) { fo[NA + 6 * lane + i] = F[i]; fo[NA + 6 * lane + 3 + i] = Mo[i]; }
+            }
+            if (lane < T::NL) fo[NA + 6 * T::NF + lane] = lds[LY::LIM + 4 * lane];
         }
         wave_sync();
         if (obs)
@@ -2759,6 +2790,7 @@ struct bioim_handle {
     void *pert_x, *pert_y; /* apply_perturbations table: double [pert_n], Real [pert_n][n] */
     int pert_n, pert_ob;
     void *final_obs;    /* caller's device buffer [n][obs_stride] or null (bioim_set_final_obs) */
+    void *force_out;    /* caller's device buffer [n][force_dim] or null (bioim_set_force_report) */
     int rk;             /* integrator: 0 semi-implicit substeps (pack nsub), 1 RK-Merson (bioim_set_integrator) */
     double rk_acc;
     Ops ops;
@@ -2787,6 +2819,8 @@ LaunchArgs<T, Real> make_args(bioim_handle_t *h, int mode, const void *actions, 
     a.actions = reinterpret_cast<const Real *>(actions);
     a.obs = reinterpret_cast<Real *>(obs);
     a.final_obs = mode == 0 ? reinterpret_cast<Real *>(h->final_obs) : nullptr;
+    a.force_out = reinterpret_cast<Real *>(h->force_out);
+    a.force_dim = h->nact + 6 * h->pack.ncforce + h->pack.nlimit;   /* bioim_force_report_dim */
     a.reward = reinterpret_cast<Real *>(reward);
     a.info = reinterpret_cast<Real *>(info);
     a.done_out = done;
@@ -3077,6 +3111,17 @@ int bioim_set_integrator(bioim_handle_t *h, int kind, double accuracy) {
         return fail(BIOIM_E_ARG, "bioim_set_integrator: kind 0 (semi-implicit) or 1 (RK-Merson, accuracy > 0)");
     h->rk = kind;
     h->rk_acc = kind == 1 ? accuracy : 0.0;
+    return 0;
+}
+
+int bioim_force_report_dim(const bioim_handle_t *h) {
+    if (!h) return fail(BIOIM_E_ARG, "null handle");
+    return h->nact + 6 * h->pack.ncforce + h->pack.nlimit;
+}
+
+int bioim_set_force_report(bioim_handle_t *h, void *force_out) {
+    if (!h) return fail(BIOIM_E_ARG, "null handle");
+    h->force_out = force_out;
     return 0;
 }
 

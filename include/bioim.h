@@ -152,6 +152,15 @@ int bioim_set_integrator(bioim_handle_t *h, int kind, double accuracy);
  * bootstrapping in the reference's jaxrl SAC loop,
  * tests/sample_baselines_training.py:69-91).  NULL disables it. */
 int bioim_set_final_obs(bioim_handle_t *h, void *final_obs);
+/* Optional per-force-element report (the reference's ForceReporter analysis,
+ * opensim_wrapper.py:10-15, printed by save_simulation :334-338): when set,
+ * every realize writes per env a row of bioim_force_report_dim() values:
+ * [actuation of each muscle (tendon force, N) or coordinate actuator
+ * (control x optimal force)] [per Hunt-Crossley force: force (3) and moment
+ * about the ground origin (3) on the feet] [per CoordinateLimitForce: its
+ * generalized force].  NULL disables it. */
+int bioim_force_report_dim(const bioim_handle_t *h);
+int bioim_set_force_report(bioim_handle_t *h, void *force_out);
 /* Sum over the handle's envs of their reset counters (explicit resets and
  * in-kernel auto-resets); synchronizes the handle's streams.  Lets a caller
  * count terminations over a stretch of steps without touching the step

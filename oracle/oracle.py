@@ -52,6 +52,7 @@ class Oracle:
                                          C.POINTER(C.c_int32), _dp, C.c_int]),
             ('orc_env_set_integrator', C.c_int, [C.c_void_p, C.c_int, C.c_double]),
             ('orc_env_rk_stats', None, [C.c_void_p, _dp]),
+            ('orc_force_report', C.c_int, [C.c_void_p, C.c_void_p, _dp]),
         ]:
             f = getattr(L, name)
             f.restype = res
@@ -106,6 +107,13 @@ class Oracle:
         """(accepted steps, rejected steps, smallest step, next step) since set_integrator"""
         out = np.zeros(4)
         self.lib.orc_env_rk_stats(self.env_ptr(envs, i), _ptr(out))
+        return out
+
+    def force_report(self, envs, i):
+        """per-force-element values of env i's realized state (bioim_set_force_report layout)"""
+        pk = self.pack
+        out = np.zeros(pk.nact + 6 * pk.ncforce + pk.nlimit)
+        self.lib.orc_force_report(self.pk, self.env_ptr(envs, i), _ptr(out))
         return out
 
     def state_dim(self):

@@ -75,7 +75,7 @@ def test_trajectory_recorder_writes_opensim_storage(tmp_path):
     pk, names = load_pack(env_id), load_names(env_id)
     rec = TrajectoryRecorder(pk, names)
     rng = np.random.default_rng(0)
-    dim = 5 + 2 * pk.ndof + 2 * pk.nmuscle + pk.horizon * pk.nact + pk.nact
+    dim = 5 + 2 * pk.ndof + 2 * pk.nmuscle + pk.horizon * pk.nact + pk.nact + 1
     rows = []
     for k in range(4):
         s = rng.normal(size=dim)
@@ -131,13 +131,28 @@ def test_single_env_save_simulation_and_perturbation(tmp_path):
     random.seed(1)
     orc.reset(bufs, 0, random.randint(0, pk.reset_hi))
     states = [orc.get_state(bufs, 0)]
+    forces = [orc.force_report(bufs, 0)]
     for t in range(6):
         a = np.array([pk.ref_q[min(env.osim_model.istep + 1, pk.nrows - 1)][pk.pd_coord[i]] for i in range(pk.nact)])
         o, r, d, _ = env.step(a)
         ro, rr, rd, _ = orc.step(bufs, 0, a)
         np.testing.assert_allclose(o, ro, rtol=1e-7, atol=1e-7)
         states.append(orc.get_state(bufs, 0))
+        forces.append(orc.force_report(bufs, 0))
     paths = env.osim_model.save_simulation(str(tmp_path))
+    # ForceReporter (opensim_wrapper.py:10-15, :338): actuators, ground-side contact records, limit forces
+    hf, lf, df = read_sto(paths['forces'])
+    fr = np.array(forces)
+    nf = pk.nact + 6 * pk.ncforce + pk.nlimit
+    assert df.shape == (7, 1 + nf) and lf[0] == 'time'
+    names = load_names(env_id)
+    assert lf[1 + pk.nact:1 + pk.nact + 6] == [f'{names["cforces"][0]}.ground.{k}.{x}' for k in ('force', 'torque')
+                                                for x in 'XYZ']
+    np.testing.assert_allclose(df[:, 1:1 + pk.nact], fr[:, :pk.nact], rtol=1e-7, atol=1e-6)
+    np.testing.assert_allclose(df[:, 1 + pk.nact:1 + pk.nact + 6 * pk.ncforce], -fr[:, pk.nact:pk.nact + 6 * pk.ncforce],
+                               rtol=1e-6, atol=1e-4)
+    np.testing.assert_allclose(df[:, -pk.nlimit:], fr[:, -pk.nlimit:], rtol=1e-6, atol=1e-6)
+    assert np.abs(df[:, 1 + pk.nact:1 + pk.nact + 6 * pk.ncforce]).max() > 1.0     # feet on the ground
     h, labels, data = read_sto(paths['states'])
     assert data.shape[0] == 7
     np.testing.assert_allclose(data[:, 0], [s[0] for s in states], atol=1e-9)
