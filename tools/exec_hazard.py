@@ -68,23 +68,25 @@ def scan(ins):
             continue
         if not dst or not src:
             continue
-        start = stack[0][1]
-        # source defined before the outermost open region (not written inside it before i)
-        if any(s in d for j in range(start, i) for d in [ins[j][1]] for s in src):
+        inner_sv, start = stack[-1]
+        # source defined before the innermost open region (not written inside it before i)
+        if any(sr in ins[j][1] for j in range(start, i) for sr in src):
             continue
-        # destination read after the region closes (first later access is a read)
-        depth = len(stack)
-        j, d = i + 1, depth
+        # the destination already holds the value in every lane: its last write before the
+        # region is the same copy and the source was not rewritten since (a redundant re-copy)
+        lw = next((j for j in range(start - 1, -1, -1) if any(d in ins[j][1] for d in dst)), None)
+        if lw is not None and ins[lw][0] == op and ins[lw][2] == src and \
+                not any(sr in ins[j][1] for j in range(lw + 1, start) for sr in src):
+            continue
+        # destination read after THIS region's join (s_or_b64 exec, exec, <its saved mask>)
+        # before being rewritten
+        j = i + 1
         closed = False
         verdict = None
         while j < len(ins) and verdict is None:
             o, dd, ss, rr = ins[j]
-            if o in ('s_and_saveexec_b64', 's_or_saveexec_b64', 's_andn2_saveexec_b64'):
-                d += 1
-            elif o == 's_or_b64' and rr.split(None, 1)[1].startswith('exec, exec,'):
-                d -= 1
-                if d < depth:
-                    closed = True
+            if o == 's_or_b64' and rr.split(None, 1)[1].startswith('exec, exec,') and rr.split(',')[-1].strip() == inner_sv:
+                closed = True
             if any(x in ss for x in dst):
                 verdict = 'read-after-join' if closed else 'read-inside'
             elif any(x in dd for x in dst):
