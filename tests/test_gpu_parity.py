@@ -513,3 +513,84 @@ def test_rk_merson_parity_fp64(env_id):
           f'{100 * frac:.1f} % <= 1e-8, median {np.median(errs):.1e}; q\'\' {qerr:.1e}; state {serr:.1e}')
     assert errs.max() < 1e-4 and serr < 1e-4 and frac >= 0.95 and qerr < 1e-2
     env.close()
+
+
+def tracking_actions(pk, states, kp=1500.0, kd=80.0):
+    """A reference-tracking policy for the torque IDs: each actuator's torque
+    is a stiff PD on the coordinate it drives, toward the reference row
+    istep + 1, expressed as the PD target the env expects
+    (torque_walking_imitation_env3D.py:125-139: tau = Kp (a - x) - Kv v with
+    the reference's index quirk on x and v, inverted here).  With horizon 1
+    the torque is applied as computed."""
+    acts = np.zeros((len(states), pk.nact))
+    nd = pk.ndof
+    for k, s in enumerate(states):
+        q, u, r = s[5:5 + nd], s[5 + nd:5 + 2 * nd], min(int(s[1]) + 1, pk.nrows - 1)
+
+        def qv(c):
+            d = pk.coord[c].dof
+            return q[d] if d >= 0 else pk.coord[c].default_value
+
+        def uv(c):
+            d = pk.coord[c].dof
+            return u[d] if d >= 0 else 0.0
+        for i in range(pk.nact):
+            ca = pk.coordact[i].coord
+            tau = kp * (pk.ref_q[r][ca] - qv(ca)) + kd * (pk.ref_u[r][ca] - uv(ca))
+            acts[k, i] = qv(pk.pd_coord[i]) + (tau + pk.kv[i] * uv(pk.pd_vcoord[i])) / pk.kp[i]
+    return acts
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+@pytest.mark.parametrize('env_id', ['TorqueRunningImitation3D-v0', 'TorqueWalkingImitation3D-v0'])
+def test_parity_200_steps_3d_envs_kept_up(env_id):
+    """north_star's 200 identical-action steps on the spatial model with most
+    envs alive to the end: a stiff reference-tracking PD (tracking_actions,
+    config horizon=1) keeps >= 50 % of 32 envs up for all 200 steps (the
+    oracle run of this drive: 21 / 24 of 32 with the perturbed twin below).
+
+    Walking under a stiff PD held over 10 ms is chaotic: the oracle against
+    itself, started one ulp apart in one coordinate, drifts 4.5e-8 by t = 50,
+    1e-5 by t = 85 and O(1) by t = 150-200 (the twin curve, computed here).
+    No two fp64 implementations can then stay within 1e-4 over 200 steps;
+    what the HIP path must do is not diverge faster than that.  Bounds: obs
+    and reward within 1e-4 relative (north_star) and equal `done` for the
+    first 60 steps; afterwards, on envs alive on both sides, GPU-vs-oracle
+    error at most 1e4 x the twin's (or 1e-4); >= 50 % of the GPU's envs alive
+    at t = 200.  Actions come from the oracle's state and go to all sides."""
+    import torch
+    n, T, cfg = 32, 200, {'horizon': 1}
+    pk, env, orc, bufs = _setup(env_id, n, 64, config=cfg)
+    twin = orc.new_envs(n)
+    rng = np.random.default_rng(7)
+    rows = rng.integers(0, min(pk.reset_hi, pk.n_episode - T) + 1, size=n)
+    env.reset(ref_index=rows)
+    for i in range(n):
+        orc.reset(bufs, i, int(rows[i]))
+        orc.reset(twin, i, int(rows[i]))
+        s = orc.get_state(twin, i)
+        s[5] = np.nextafter(s[5], np.inf)        # one ulp in the first coordinate
+        orc.set_state(twin, i, s)
+    live = np.ones(n, bool)                      # alive on the oracle and the GPU
+    gpu_alive = np.ones(n, bool)
+    e_gpu, e_twin = np.zeros(T), np.zeros(T)
+    for t in range(T):
+        acts = tracking_actions(pk, [orc.get_state(bufs, i) for i in range(n)])
+        obs, rew, done = (v.cpu().numpy() for v in env.step(torch.as_tensor(acts, device=env.device))[:3])
+        gpu_alive &= ~done.astype(bool)
+        for i in np.where(live)[0]:
+            o, r, d, _ = orc.step(bufs, i, acts[i])
+            o2, r2, d2, _ = orc.step(twin, i, acts[i])
+            e = max(_rel(obs[i], o).max(), abs(rew[i] - r) / max(1.0, abs(r)))
+            e_gpu[t] = max(e_gpu[t], e)
+            e_twin[t] = max(e_twin[t], _rel(o2, o).max(), abs(r2 - r) / max(1.0, abs(r)))
+            if t < 60:
+                assert e < 1e-4, (t, i, e)
+                assert bool(done[i]) == d, (t, i)
+            live[i] = not (d or d2 or done[i])
+    ks = [0, 24, 49, 84, 99, 149, 199]
+    print(f'{env_id} 200 steps, tracking drive: GPU alive at t=200 {gpu_alive.sum()}/{n}; max rel err GPU vs oracle / '
+          f'oracle vs its one-ulp twin at t=' + ', '.join(f'{k + 1}: {e_gpu[k]:.1e} / {e_twin[k]:.1e}' for k in ks))
+    assert (e_gpu[60:] <= np.maximum(1e-4, 1e4 * e_twin[60:])).all(), np.argmax(e_gpu[60:] / np.maximum(1e-30, e_twin[60:]))
+    assert gpu_alive.sum() >= n // 2
+    env.close()
