@@ -1,0 +1,262 @@
+"""Dynamics pinned to OpenSim's own output: the StaticOptimization results the
+reference ships (tests/golden/make_so_fixtures.py -> tests/golden/so_3D.npz).
+
+OpenSim's StaticOptimization (setup_so.xml: use_muscle_physiology, rigid
+tendons, coordinates low-passed at 6 Hz, measured GRFs low-passed at 6 Hz,
+model/reserve_actuators.xml appended) finds, at every 0.01 s frame,
+activations a_m and reserve / residual controls such that the actuators
+produce the model's inverse-dynamics generalized forces under the GRFs.  On
+OUR compiled model (the oracle's mass matrix, bias and gravity, our joint
+kinematics, path lengths and moment arms, our Millard curves) the same
+balance is evaluated with OpenSim's a_m and controls:
+
+    tau_ID = M(q) q'' + c(q, q') - g(q) - J^T F_grf
+    tau_SO = sum_m -F_m dL_m/dq + reserves + residual actuators,
+    F_m    = F0 a_m fal(l~) fv(v~) cos(alpha)     (fiber state: see below)
+
+and the two must agree.  They are two independent computations: tau_ID
+uses only the skeleton (masses, inertias, frames) and the GRFs; tau_SO only
+the muscles (paths, curves, F0, pennation) and OpenSim's solution.  The
+filtering and differentiation of q are restated (3rd-order Butterworth run
+forward and backward, quintic interpolating splines), not OpenSim's code,
+so q'' — hence tau_ID — carries some disagreement; the bounds below leave
+room for it and the mutation tests show the check still bites.
+
+Fiber state.  Which muscle force OpenSim's SO applies is read off the data
+(python tests/test_so_pin.py prints the table; RMS(tau_ID - tau_SO) /
+RMS(tau_ID) over the 8 leg joints):
+    fiber length from the compliant-tendon static equilibrium at the SO
+    activation (our env's own reset equilibrium, passive force included in
+    it), force = active fiber force a*F0*fal*fv*cos(alpha) only   0.049-0.171
+    rigid tendon, active only                                     0.048-0.409
+    rigid tendon, active + passive                                0.41 -4.1
+    equilibrium, active + passive                                 0.32 -2.6
+i.e. the SO's constraint carries the active fiber force at the equilibrated
+fiber state and not the passive one; the first reading is the one used.
+"""
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _filtered_spline(t, x, fc):
+    from scipy.interpolate import make_interp_spline
+    from scipy.signal import butter, filtfilt
+    dt = t[1] - t[0]
+    b, a = butter(3, fc / (0.5 / dt))
+    pad = len(t) // 2
+    y = filtfilt(b, a, x, axis=0, padtype='odd', padlen=pad)
+    return make_interp_spline(t, y, k=5, axis=0)
+
+
+class SOBalance:
+    def __init__(self, oracle_lib, z, mutate=None, passive=False, fiber='equilibrium'):
+        self.passive, self.fiber = passive, fiber
+        from bioimitation.obslayout import load_names
+        from bioimitation.registry import load_pack
+        self.z = z
+        self.pk = load_pack(str(z['env_id']))
+        self.names = load_names(str(z['env_id']))
+        if mutate:
+            mutate(self.pk, self.names)
+        self.orc = oracle_lib.Oracle(self.pk)
+        pk = self.pk
+        self.dof = np.array([pk.coord[c].dof for c in range(pk.ncoord)])
+        self.free = np.where(self.dof >= 0)[0]
+        self.q_spl = _filtered_spline(z['ik_time'], z['ik_q'], float(z['coord_cutoff']))
+        from scipy.interpolate import make_interp_spline
+        g = z['grf'].reshape(len(z['grf']), -1)
+        self.g_spl = make_interp_spline(z['grf_time'], g, k=3, axis=0)
+        self.bodies = self.names['bodies']
+        self.mus = [self.names['muscles'].index(str(n)) if k == 'muscle' else -1
+                    for n, k in zip(z['so_names'], z['act_kind'])]
+
+    def _qd(self, qc):
+        out = np.zeros(self.pk.ndof)
+        out[self.dof[self.free]] = qc[self.free]
+        return out
+
+    def _frames(self, qd):
+        R, p, _ = self.orc.fk(qd)
+        return R, p
+
+    def _body_jacobian(self, qd, b, P):
+        """d(point P fixed in body b)/dq and the body's angular velocity per dof (ground)."""
+        R0, p0 = self._frames(qd)
+        Pb = R0[b].T @ (P - p0[b])
+        Jv = np.zeros((3, len(qd)))
+        Jw = np.zeros((3, len(qd)))
+        h = 1e-7
+        for d in range(len(qd)):
+            qp, qm = qd.copy(), qd.copy()
+            qp[d] += h
+            qm[d] -= h
+            Rp, pp = self._frames(qp)
+            Rm, pm = self._frames(qm)
+            Jv[:, d] = ((pp[b] + Rp[b] @ Pb) - (pm[b] + Rm[b] @ Pb)) / (2 * h)
+            W = ((Rp[b] - Rm[b]) / (2 * h)) @ R0[b].T
+            Jw[:, d] = [W[2, 1], W[0, 2], W[1, 0]]
+        return Jv, Jw
+
+    def muscle_force(self, q, u, m, a):
+        """Tendon force of muscle m at activation a as OpenSim's SO applies it
+        (module docstring, 'fiber state'); leaves dL/dq in self._dL."""
+        mu, orc = self.pk.muscle[m], self.orc
+        L, Ld, self._dL = orc.muscle_path(q, u, m)
+        w = mu.lopt * np.sin(mu.alpha_opt)
+        if self.fiber == 'rigid':
+            lt = L - mu.lts
+            lm = np.sqrt(lt * lt + w * w)
+        else:
+            lm = orc.muscle_equilibrium(m, a, L)
+        cosa = np.sqrt(lm * lm - w * w) / lm
+        fal = orc.curve(m, 0, lm / mu.lopt)[0]
+        fv = orc.curve(m, 1, Ld * cosa / (mu.lopt * mu.vmax))[0]
+        fpe = orc.curve(m, 2, lm / mu.lopt)[0] if self.passive else 0.0
+        return mu.fiso * (a * fal * fv + fpe) * cosa
+
+    def frame(self, t):
+        """(tau_ID, tau_SO) per dof at SO time t."""
+        z, pk, orc = self.z, self.pk, self.orc
+        qc, uc, ac = self.q_spl(t), self.q_spl.derivative(1)(t), self.q_spl.derivative(2)(t)
+        q, u, a = self._qd(qc), self._qd(uc), self._qd(ac)
+        tau_id = orc.id_eval(2, q, u, a) + orc.id_eval(1, q, u) - orc.id_eval(0, q)
+        grf = self.g_spl(t).reshape(-1, 9)
+        for k, body in enumerate(z['grf_bodies']):
+            F, P, T = grf[k, :3], grf[k, 3:6], grf[k, 6:]
+            if not np.any(F) and not np.any(T):
+                continue
+            Jv, Jw = self._body_jacobian(q, self.bodies.index(str(body)), P)
+            tau_id -= Jv.T @ F + Jw.T @ T
+        i = np.searchsorted(z['so_time'], t - 1e-9)
+        ctrl = z['so_values'][i]
+        tau_so = np.zeros(pk.ndof)
+        for j, kind in enumerate(z['act_kind']):
+            c = ctrl[j]
+            if kind == 'muscle':
+                tau_so -= self.muscle_force(q, u, self.mus[j], c) * self._dL
+            elif kind == 'CoordinateActuator':
+                d = self.dof[int(z['act_coord'][j])]
+                if d >= 0:
+                    tau_so[d] += c * z['act_opt'][j]
+            else:
+                b = self.bodies.index(str(z['act_body'][j]))
+                R0, p0 = self._frames(q)
+                vec = z['act_dir'][j] * c * z['act_opt'][j]
+                if not z['act_vec_global'][j]:
+                    vec = R0[b] @ vec
+                if kind == 'PointActuator':
+                    P = z['act_point'][j] if z['act_point_global'][j] else p0[b] + R0[b] @ z['act_point'][j]
+                    Jv, _ = self._body_jacobian(q, b, P)
+                    tau_so += Jv.T @ vec
+                else:
+                    _, Jw = self._body_jacobian(q, b, p0[b])
+                    tau_so += Jw.T @ vec
+        return tau_id, tau_so
+
+
+def balance(oracle_lib, mutate=None, stride=1, passive=False, fiber='equilibrium'):
+    z = dict(np.load(os.path.join(HERE, 'golden', 'so_3D.npz'), allow_pickle=False))
+    so = SOBalance(oracle_lib, z, mutate, passive, fiber)
+    ts = z['so_time'][::stride]
+    ids, sos = zip(*(so.frame(t) for t in ts))
+    return so, np.array(ids), np.array(sos)
+
+
+JOINTS = ['hip_flexion_r', 'hip_adduction_r', 'knee_angle_r', 'ankle_angle_r',
+          'hip_flexion_l', 'hip_adduction_l', 'knee_angle_l', 'ankle_angle_l']
+PELVIS = ['pelvis_tilt', 'pelvis_list', 'pelvis_rotation', 'pelvis_tx', 'pelvis_ty', 'pelvis_tz']
+
+
+def errors(so, tid, tso, which):
+    out = {}
+    for c in which:
+        d = so.dof[so.names['coords'].index(c)]
+        e = tid[:, d] - tso[:, d]
+        out[c] = (np.sqrt(np.mean(e ** 2)), np.sqrt(np.mean(tid[:, d] ** 2)))
+    return out
+
+
+def ratios(so, tid, tso):
+    return {c: e / s for c, (e, s) in {**errors(so, tid, tso, JOINTS), **errors(so, tid, tso, PELVIS)}.items()}
+
+
+@pytest.fixture(scope='module')
+def model_balance(oracle_lib):
+    return balance(oracle_lib)
+
+
+def test_whole_body_balance_pelvis_residuals(model_balance):
+    """Pelvis rows: OpenSim's residual actuators absorb exactly the whole-body
+    imbalance, so these rows check every segment's mass, COM and inertia, the
+    frames, gravity and the GRF application — independent of the muscles."""
+    so, tid, tso = model_balance
+    r = ratios(so, tid, tso)
+    for c in ('pelvis_tilt', 'pelvis_list', 'pelvis_rotation'):
+        assert r[c] < 0.03, (c, r[c])          # measured 0.0040-0.0189
+    for c in ('pelvis_tx', 'pelvis_ty', 'pelvis_tz'):
+        assert r[c] < 1e-4, (c, r[c])          # measured <= 1.2e-5
+
+
+def test_joint_balance_muscles(model_balance):
+    """Joint rows: OpenSim's activations through OUR paths, moment arms and
+    Millard curves reproduce the inverse-dynamics joint moments."""
+    so, tid, tso = model_balance
+    r = ratios(so, tid, tso)
+    joints = np.array([r[c] for c in JOINTS])
+    assert joints.max() < 0.2, dict(zip(JOINTS, joints))   # measured max 0.171 (ankle_angle_r)
+    assert joints.mean() < 0.1, joints.mean()               # measured 0.083
+
+
+def _mean_joint(oracle_lib, mutate=None, **kw):
+    so, tid, tso = balance(oracle_lib, mutate, **kw)
+    r = ratios(so, tid, tso)
+    return np.mean([r[c] for c in JOINTS]), r
+
+
+def test_balance_detects_model_errors(oracle_lib, model_balance):
+    """The check bites: 5% heavier segments break the pelvis rows; 25% stronger
+    muscles, or the rigid-tendon / passive-force readings of the SO, break the
+    joint rows."""
+    so, tid, tso = model_balance
+    base = np.mean([ratios(so, tid, tso)[c] for c in JOINTS])
+
+    def heavier(pk, names):
+        for b in range(pk.ncbody):
+            pk.cbody[b].mass *= 1.05
+
+    def stronger(pk, names):
+        for m in range(pk.nmuscle):
+            pk.muscle[m].fiso *= 1.25
+    _, r = _mean_joint(oracle_lib, heavier)
+    assert r['pelvis_ty'] > 0.2 and r['pelvis_tilt'] > 0.1, r
+    assert _mean_joint(oracle_lib, stronger)[0] > 2 * base
+    assert _mean_joint(oracle_lib, fiber='rigid')[0] > 2 * base
+    assert _mean_joint(oracle_lib, passive=True)[0] > 10 * base
+
+
+if __name__ == '__main__':
+    import sys
+    import time
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), 'bioimitation-gym_amd'))
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), 'oracle'))
+    import oracle as orc_mod
+
+    def heavier(pk, names):
+        for b in range(pk.ncbody):
+            pk.cbody[b].mass *= 1.05
+
+    def stronger(pk, names):
+        for m in range(pk.nmuscle):
+            pk.muscle[m].fiso *= 1.25
+    cases = {'model': (None, {}), 'rigid': (None, dict(fiber='rigid')),
+             'rigid+fpe': (None, dict(fiber='rigid', passive=True)), 'equil+fpe': (None, dict(passive=True)),
+             'mass x1.05': (heavier, {}), 'F0 x1.25': (stronger, {})}
+    for k, (mut, kw) in cases.items():
+        t0 = time.time()
+        so, tid, tso = balance(orc_mod, mut, **kw)
+        r = ratios(so, tid, tso)
+        print(f'{k:12s} ' + ' '.join(f'{c}={v:.4f}' for c, v in r.items()), f'({time.time() - t0:.1f}s)')
