@@ -140,11 +140,16 @@ def main():
     ap.add_argument('--env-id', default='MuscleWalkingImitation2D-v0')
     ap.add_argument('--integrator', default='semi-implicit', choices=['semi-implicit', 'rk-merson'],
                     help="'rk-merson': the reference's adaptive integrator at accuracy 1e-3 (DESIGN.md §3)")
+    ap.add_argument('--rk-budget', type=int, default=0,
+                    help='rk-merson only: attempts per env per launch (bioim_set_rk_budget); value counts the env '
+                         'steps that finished')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--mixed', default=None,
                     help="mixed batch 'ID_A,ID_B' split 50/50 per GPU (BASELINE config C5), e.g. "
                          "MuscleLockedKneeImitation3D-v0,MusclePalsyImitation3D-v0")
     a = ap.parse_args()
+    if a.rk_budget and (a.integrator != 'rk-merson' or a.mixed):
+        ap.error('--rk-budget needs --integrator rk-merson and a single env id')
 
     if 'WORLD_SIZE' not in os.environ and a.gpus > 1:
         sys.exit(_spawn_ranks(a))
@@ -184,6 +189,8 @@ def main():
         env = VectorEnv(a.env_id, a.envs, config={'integrator': a.integrator}, device=local, precision=a.precision,
                         seed=1000, auto_reset=True, env_offset=rank * a.envs)   # global env index block (parallel.py)
         handles = [env]
+        if a.rk_budget:
+            env.set_rk_budget(a.rk_budget)
     n, A = a.envs, env.action_dim
     pool = 64      # action batches cycled through (uploaded once; inputs resident in HBM)
     gen = np.random.Generator(np.random.PCG64(rank))
@@ -200,9 +207,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    finished = torch.zeros(n, dtype=torch.int32, device=dev) if a.rk_budget else None
     ev0.record(stream)
     for k in range(a.steps):
         env.step(acts[(a.burn_in + a.warmup + k) % pool])
+        if finished is not None:
+            finished += env.ready   # envs whose step finished in this launch (one small add per launch)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
@@ -214,9 +224,15 @@ def main():
         tt = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt[0])
-    done_rate = (sum(h.reset_count() for h in handles) - resets0) / (n * a.steps)
-    steps_total = world * n * a.steps
+    steps_local = int(finished.sum()) if finished is not None else n * a.steps
+    if dist:
+        st_ = torch.tensor([steps_local], dtype=torch.float64)
+        dist.all_reduce(st_)
+        steps_total = float(st_[0])
+    else:
+        steps_total = steps_local
     value = steps_total / t_max
+    done_rate = (sum(h.reset_count() for h in handles) - resets0) / max(steps_local, 1)
     if rank == 0:
         real_bytes = 8 if a.precision == 64 else 4
         if a.mixed:   # env-weighted mean over the segments
@@ -242,7 +258,7 @@ def main():
             'data': 'synthetic: PCG64 U[0,1] muscle excitations; reference motion synthesized from the shipped 3D IK',
             'config': {'workload': f'{a.env_id} batched env.step, {n} envs/GPU, ' +
                        (f'nsub={env.nsub}' if a.integrator == 'semi-implicit' else 'RK-Merson 1e-3') + ', auto-reset',
-                       'integrator': a.integrator,
+                       'integrator': a.integrator, 'rk_budget': a.rk_budget or None,
                        'envs_per_gpu': n, 'lanes_per_env': env.lanes_per_env, 'parallelism': f'env-shard x{world}',
                        'launch': env.launch},
             'roofline': roofline,
@@ -250,6 +266,8 @@ def main():
         valu = _profile_record('valu.json', key)
         if valu:   # the bound that is live for this kernel, from the rocprofv3 SQ passes
             line['valu'] = valu
+        if a.rk_budget:
+            line['finished_env_steps'] = steps_total
         if not a.no_cpu_baseline and world == 1:
             line['cpu_baseline'] = cpu_baseline(a.env_id)
         print(json.dumps(line), flush=True)

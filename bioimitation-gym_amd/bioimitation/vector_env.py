@@ -128,6 +128,28 @@ class VectorEnv:
             self.force_report = None
         _lib.check(self._L.bioim_set_force_report(self._h, self._ptr(self.force_report)))
 
+    def set_rk_budget(self, attempts: int):
+        """Budgeted steps for the 'rk-merson' integrator (``bioim_set_rk_budget``):
+        each ``step()`` gives every env at most ``attempts`` Kutta-Merson step
+        attempts; an env not finished by then resumes in the next ``step()``
+        (its action row is ignored until then) and is 0 in ``self.ready``.
+        Only ready rows of obs / reward / done / info are fresh.  The
+        trajectories equal the unbudgeted run's bit for bit; a launch is no
+        longer as long as its stiffest env.  ``attempts=0`` turns it off."""
+        import torch
+        if self.integrator != 'rk-merson' and attempts:
+            raise ValueError("set_rk_budget needs config integrator='rk-merson'")
+        self.rk_budget = int(attempts)
+        if attempts and getattr(self, 'ready', None) is None:
+            self.ready = torch.ones(self.num_envs, dtype=torch.uint8, device=self.device)
+        elif not attempts:
+            self.ready = None
+        _lib.check(self._L.bioim_set_rk_budget(self._h, self.rk_budget, self._ptr(self.ready)))
+
+    def pending_count(self) -> int:
+        """Envs suspended mid-step by the RK budget."""
+        return _lib.check(self._L.bioim_pending_count(self._h))
+
     @staticmethod
     def _ptr(t):
         return C.c_void_p(t.data_ptr()) if t is not None else None

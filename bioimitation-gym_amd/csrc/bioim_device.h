@@ -222,4 +222,12 @@ struct DState {
     double *t;
     int32_t *istep, *has_last, *done, *resets;
     double *hrk;   /* [N] RK-Merson step size carried to the next env step (0: none yet) */
+    /* budgeted RK launches (bioim_set_rk_budget): an env whose step is not
+     * finished within the launch's attempt budget is suspended at an accepted
+     * RK point and resumed by the next launch */
+    int32_t *pend;  /* [N] 1: suspended mid-step                                      */
+    double *rkt, *rkh; /* [N] its integration time and proposed step size            */
+    int32_t *rka;   /* [N] attempts spent on the step so far                          */
+    Real *ctl, *cur; /* [nact][N] its held controls and smoothed actions               */
+    Real *vnw;      /* [nm][N] fiber-velocity warm starts (the last call's roots)      */
 };

@@ -1793,6 +1793,8 @@ template <class T, typename Real> struct LaunchArgs {
     const Real *pert_y;
     int pert_n, pert_ob;
     double rk_acc;     /* RK-Merson accuracy (RK kernels) */
+    int rk_budget;     /* RK kernels: attempts per env per launch (0: finish every step) */
+    uint8_t *ready_out; /* optional [N]: 1 where the env finished its step in this launch */
 };
 
 /* Reference integrator (RK kernels): OpenSim's Manager integrates with an
@@ -1897,6 +1899,11 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     int done = 0;
     Real rew = 0, inf[5] = {0, 0, 0, 0, 0};
     bool do_reset = (mode == 1);
+    /* budgeted RK: a suspended step resumes (its action row is ignored) */
+    const bool budget = RK && a.rk_budget > 0;
+    const bool resume = RK && mode == 0 && st.pend[env] != 0;
+    bool suspend = false;
+    int launch_attempts = 0;
     int reset_row = 0;
     if (mode == 1) reset_row = a.ref_index ? a.ref_index[gidx] : draw_index(a.seed, a.env_offset + env, resets, M.reset_hi);
 
@@ -1913,7 +1920,17 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     const PertArgs<Real> PA{a.pert_x, a.pert_y, a.pert_n, a.pert_ob, env, N};
     double *pslot = reinterpret_cast<double *>(smem_raw + SMB + sizeof(Real) * EPB * LY::SIZE) + PERT_SLOT * slot;
     if (PERT && lane == 0) { pslot[0] = t; pslot[1] = 0; pslot[2] = 0; pslot[3] = -1; pslot[4] = 0; }
-    if (mode == 0) {
+    if (resume) {
+        /* the state is at the accepted RK point rk_t of the step ending at t */
+#pragma unroll
+        for (int j = 0; j < MPL; ++j) {
+            const int m = mslot<T>(lane + j * G);
+            if (m < NA) { control[j] = st.ctl[(size_t)m * N + env]; curr[j] = st.cur[(size_t)m * N + env]; }
+            if (NM > 0 && m < NM) D.ms[j].vN = st.vnw[(size_t)m * N + env];
+        }
+        rk_t = st.rkt[env]; rk_tf = t; rk_h = st.rkh[env]; rk_attempts = st.rka[env];
+        remaining = 1;
+    } else if (mode == 0) {
         /* ---- action pre-processing (Env.step) */
         Real raw[MPL];
         bool nan_here = false;
@@ -2013,8 +2030,10 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         if constexpr (RK) {
             if (remaining > 0 && rk_stage == 0) {   /* start an RK step, or stop */
                 if (!(rk_tf - rk_t > 1e-14 * (1.0 + fabs(rk_tf)))) remaining = 0;
+                else if (budget && launch_attempts >= a.rk_budget) { suspend = true; break; }
                 else if (++rk_attempts > BIOIM_RK_MAX_ATTEMPTS) { rk_fail = true; remaining = 0; }
                 else {
+                    ++launch_attempts;
                     rk_last = false;
                     if (rk_h >= rk_tf - rk_t) { rk_h = rk_tf - rk_t; rk_last = true; }
                     rk_err = 0;
@@ -2369,9 +2388,22 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         st.istep[env] = istep;
         st.has_last[env] = has_last;
         st.old_px[env] = old_px;
-        st.done[env] = (mode == 0 && !do_reset) ? done : 0;
+        st.done[env] = (mode == 0 && !do_reset && !suspend) ? done : 0;
         st.resets[env] = resets;
         if (RK || mode == 1) st.hrk[env] = rk_hnext;
+        if constexpr (RK) {
+            st.pend[env] = suspend ? 1 : 0;
+            if (suspend) { st.rkt[env] = rk_t; st.rkh[env] = rk_h; st.rka[env] = rk_attempts; a.done_out[env] = 0; }
+            if (mode == 0 && a.ready_out) a.ready_out[env] = suspend ? 0 : 1;
+        }
+    }
+    if (RK && suspend) {
+#pragma unroll
+        for (int j = 0; j < MPL; ++j) {
+            const int m = mslot<T>(lane + j * G);
+            if (m < NA) { st.ctl[(size_t)m * N + env] = control[j]; st.cur[(size_t)m * N + env] = curr[j]; }
+            if (NM > 0 && m < NM) st.vnw[(size_t)m * N + env] = D.ms[j].vN;
+        }
     }
     if (lane < ND) {
         st.q[(size_t)lane * N + env] = qd;
@@ -2793,6 +2825,8 @@ struct bioim_handle {
     void *force_out;    /* caller's device buffer [n][force_dim] or null (bioim_set_force_report) */
     int rk;             /* integrator: 0 semi-implicit substeps (pack nsub), 1 RK-Merson (bioim_set_integrator) */
     double rk_acc;
+    int rk_budget;      /* RK attempts per env per launch, 0: unbudgeted (bioim_set_rk_budget) */
+    uint8_t *ready_out; /* caller's device buffer [n] or null */
     Ops ops;
     bioim_modelpack_t pack;
 };
@@ -2830,6 +2864,8 @@ LaunchArgs<T, Real> make_args(bioim_handle_t *h, int mode, const void *actions, 
     a.pert_y = reinterpret_cast<const Real *>(h->pert_y);
     a.pert_n = h->pert_n; a.pert_ob = h->pert_ob;
     a.rk_acc = h->rk_acc;
+    a.rk_budget = h->rk ? h->rk_budget : 0;
+    a.ready_out = mode == 0 ? h->ready_out : nullptr;
     return a;
 }
 
@@ -2913,12 +2949,19 @@ template <typename Real> size_t state_layout(bioim_handle_t *h, char *base, DSta
     size_t opx = take(sizeof(Real) * n), ot = take(sizeof(double) * n);
     size_t oi = take(sizeof(int32_t) * n), ohl = take(sizeof(int32_t) * n), od = take(sizeof(int32_t) * n),
            orr = take(sizeof(int32_t) * n), ohr = take(sizeof(double) * n);
+    const size_t na1 = h->nact ? h->nact : 1, nm1 = h->nmuscle ? h->nmuscle : 1;
+    size_t opd = take(sizeof(int32_t) * n), ork = take(sizeof(double) * n), orh = take(sizeof(double) * n),
+           ora = take(sizeof(int32_t) * n), octl = take(sizeof(Real) * na1 * n), ocur = take(sizeof(Real) * na1 * n),
+           ovn = take(sizeof(Real) * nm1 * n);
     if (st) {
         st->q = (Real *)(base + oq); st->u = (Real *)(base + ou); st->act = (Real *)(base + oa);
         st->lce = (Real *)(base + ol); st->hist = (Real *)(base + oh); st->last = (Real *)(base + olast);
         st->old_px = (Real *)(base + opx); st->t = (double *)(base + ot); st->istep = (int32_t *)(base + oi);
         st->has_last = (int32_t *)(base + ohl); st->done = (int32_t *)(base + od); st->resets = (int32_t *)(base + orr);
         st->hrk = (double *)(base + ohr);
+        st->pend = (int32_t *)(base + opd); st->rkt = (double *)(base + ork); st->rkh = (double *)(base + orh);
+        st->rka = (int32_t *)(base + ora); st->ctl = (Real *)(base + octl); st->cur = (Real *)(base + ocur);
+        st->vnw = (Real *)(base + ovn);
     }
     return off;
 }
@@ -2977,6 +3020,7 @@ template <typename Real> int xfer_state(bioim_handle_t *h, double *host, const d
                 for (int i = 0; i < na; ++i) hs.hist[(hh * na + i) * n + e] = (Real)s[k++];
             for (int i = 0; i < na; ++i) hs.last[i * n + e] = (Real)s[k++];
             hs.hrk[e] = s[k++];
+            hs.pend[e] = 0;   /* a state set from outside is at a step boundary */
         }
     }
     if (in) HIPCHK(hipMemcpy(h->state_buf, buf.data(), h->state_bytes, hipMemcpyHostToDevice));
@@ -3109,9 +3153,34 @@ int bioim_set_auto_reset(bioim_handle_t *h, int on) {
 int bioim_set_integrator(bioim_handle_t *h, int kind, double accuracy) {
     if (!h || kind < 0 || kind > 1 || (kind == 1 && !(accuracy > 0)))
         return fail(BIOIM_E_ARG, "bioim_set_integrator: kind 0 (semi-implicit) or 1 (RK-Merson, accuracy > 0)");
+    if (kind != h->rk) {
+        const int np = bioim_pending_count(h);
+        if (np < 0) return np;
+        if (np > 0) return fail(BIOIM_E_ARG, "bioim_set_integrator: envs are suspended mid-step (bioim_set_rk_budget)");
+    }
     h->rk = kind;
     h->rk_acc = kind == 1 ? accuracy : 0.0;
     return 0;
+}
+
+int bioim_set_rk_budget(bioim_handle_t *h, int attempts, uint8_t *ready_out) {
+    if (!h || attempts < 0) return fail(BIOIM_E_ARG, "bioim_set_rk_budget: null handle or negative budget");
+    h->rk_budget = attempts;
+    h->ready_out = ready_out;
+    return 0;
+}
+
+int bioim_pending_count(bioim_handle_t *h) {
+    if (!h) return fail(BIOIM_E_ARG, "null handle");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    std::vector<int32_t> p(h->n);
+    const int32_t *dp = h->precision == 64 ? reinterpret_cast<DState<double> *>(h->dstate)->pend
+                                           : reinterpret_cast<DState<float> *>(h->dstate)->pend;
+    HIPCHK(hipMemcpy(p.data(), dp, sizeof(int32_t) * h->n, hipMemcpyDeviceToHost));
+    int c = 0;
+    for (int32_t v : p) c += v != 0;
+    return c;
 }
 
 int bioim_force_report_dim(const bioim_handle_t *h) {

@@ -145,6 +145,23 @@ int bioim_set_state(bioim_handle_t *h, const double *host_state);
  * oracle/bioim_oracle.c integrate_rk_merson.  Replaces the integrator
  * choice inside OsimModel.reset_manager. */
 int bioim_set_integrator(bioim_handle_t *h, int kind, double accuracy);
+/* Budgeted steps for the adaptive integrator (kind 1).  attempts > 0: each
+ * bioim_step gives every env at most `attempts` Kutta-Merson step attempts;
+ * an env whose env step is not finished by then is suspended at its last
+ * accepted integration point and resumed by the next bioim_step (its action
+ * row is ignored until it finishes).  ready_out (device [n], may be NULL)
+ * receives 1 for the envs whose step finished in this launch — only their
+ * obs / reward / done / info rows are written (done is 0 for the others).
+ * A resumed step continues bit for bit as if it had never been suspended
+ * (state, step size, attempt count and the fiber-velocity warm starts are
+ * saved), so the trajectories equal the unbudgeted run's; what changes is
+ * that one stiff env no longer holds the whole launch.  The consumer pattern
+ * is RLlib's BaseEnv.poll() / send_actions(): new actions only for ready
+ * envs.  attempts = 0 restores one-step-per-launch.  No reference
+ * counterpart (OpenSim steps one env at a time). */
+int bioim_set_rk_budget(bioim_handle_t *h, int attempts, uint8_t *ready_out);
+/* envs suspended mid-step (synchronizes the handle's stream) */
+int bioim_pending_count(bioim_handle_t *h);
 /* Optional terminal-observation output: when set (a device buffer with the
  * handle's obs row stride), every step also writes each env's observation
  * as computed by that step *before* an in-kernel auto-reset replaces it, so

@@ -1,0 +1,96 @@
+"""Budgeted steps of the reference integrator (bioim_set_rk_budget,
+include/bioim.h): an env whose Kutta-Merson step does not finish within the
+launch's attempt budget is suspended at an accepted integration point and
+resumed by the next launch.  The consumer feeds each env its own next action
+only when it is ready (RLlib BaseEnv.poll / send_actions).  Every env's
+trajectory must equal the unbudgeted run's bit for bit."""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_sync(env_id, n, T, acts, rows):
+    import torch
+    from bioimitation.vector_env import VectorEnv
+    env = VectorEnv(env_id, n, config={'integrator': 'rk-merson'}, precision=64)
+    env.reset(ref_index=rows)
+    out = []
+    for k in range(T):
+        o, r, d, _ = env.step(torch.as_tensor(acts[k], device=env.device))
+        out.append((o.cpu().numpy().copy(), r.cpu().numpy().copy(), d.cpu().numpy().copy()))
+    env.close()
+    return out
+
+
+def _run_budget(env_id, n, T, acts, rows, budget):
+    import torch
+    from bioimitation.vector_env import VectorEnv
+    env = VectorEnv(env_id, n, config={'integrator': 'rk-merson'}, precision=64)
+    env.set_rk_budget(budget)
+    env.reset(ref_index=rows)
+    k = np.zeros(n, dtype=int)
+    res_o = np.zeros((T, n, env.obs_dim))
+    res_r = np.zeros((T, n))
+    res_d = np.zeros((T, n), dtype=np.uint8)
+    launches = suspended = 0
+    while k.min() < T and launches < 40 * T:
+        a = np.stack([acts[min(k[i], T - 1)][i] for i in range(n)])
+        o, r, d, _ = env.step(torch.as_tensor(a, device=env.device))
+        ready = env.ready.cpu().numpy().astype(bool)
+        o, r, d = o.cpu().numpy(), r.cpu().numpy(), d.cpu().numpy()
+        for i in np.nonzero(ready & (k < T))[0]:
+            res_o[k[i], i], res_r[k[i], i], res_d[k[i], i] = o[i], r[i], d[i]
+        suspended += int((~ready).sum())
+        k += ready
+        launches += 1
+    pending = env.pending_count()
+    env.close()
+    return res_o, res_r, res_d, launches, suspended, pending, k
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs a HIP GPU')
+@pytest.mark.parametrize('env_id,budget', [('MuscleRunningImitation3D-v0', 6), ('TorqueWalkingImitation2D-v0', 4)])
+def test_rk_budget_equals_unbudgeted(env_id, budget):
+    from bioimitation.registry import load_pack
+    pk = load_pack(env_id)
+    n, T = 48, 12
+    rng = np.random.default_rng(7)
+    rows = rng.integers(0, 100, size=n)
+    if pk.nmuscle:
+        acts = rng.uniform(0, 0.5, size=(T, n, pk.nact))
+    else:
+        acts = np.stack([np.array([[pk.ref_q[min(int(r) + k + 1, pk.nrows - 1)][pk.pd_coord[a]] for a in range(pk.nact)]
+                                   for r in rows]) for k in range(T)]) + rng.normal(0, 0.05, size=(T, n, pk.nact))
+    ref = _run_sync(env_id, n, T, acts, rows)
+    o, r, d, launches, suspended, pending, k = _run_budget(env_id, n, T, acts, rows, budget)
+    print(f'{env_id}: budget {budget} attempts, {launches} launches for {T} steps, {suspended} suspensions, '
+          f'{pending} pending at the end')
+    assert (k >= T).all(), k
+    assert suspended > 0, 'the budget never suspended an env: the test does not exercise the resume path'
+    for t in range(T):
+        np.testing.assert_array_equal(o[t], ref[t][0], err_msg=f'obs, step {t}')
+        np.testing.assert_array_equal(r[t], ref[t][1], err_msg=f'reward, step {t}')
+        np.testing.assert_array_equal(d[t], ref[t][2], err_msg=f'done, step {t}')
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs a HIP GPU')
+def test_rk_budget_state_roundtrip_clears_pending():
+    """set_state starts every env at a step boundary; switching the integrator
+    while envs are suspended is refused."""
+    import torch
+    from bioimitation import _lib
+    from bioimitation.vector_env import VectorEnv
+    env = VectorEnv('MuscleRunningImitation3D-v0', 32, config={'integrator': 'rk-merson'}, precision=64)
+    env.set_rk_budget(1)
+    env.reset()
+    s = env.get_state()
+    env.step(torch.full((32, env.action_dim), 0.3, dtype=torch.float64, device=env.device))
+    assert env.pending_count() > 0
+    with pytest.raises(_lib.BioimError):
+        _lib.check(env._L.bioim_set_integrator(env._h, 0, 0.0))
+    env.set_state(s)
+    assert env.pending_count() == 0
+    env.close()
