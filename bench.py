@@ -197,8 +197,19 @@ def main():
     acts = torch.as_tensor(gen.uniform(0.0, 1.0, size=(pool, n, A)), dtype=env.dtype, device=dev)
     env.reset()
     stream = torch.cuda.current_stream(dev)
-    for k in range(a.burn_in + a.warmup):
-        env.step(acts[k % pool])
+    k0 = a.burn_in + a.warmup
+    if a.rk_budget:
+        # budgeted launches finish fewer than n steps each: burn in by finished env steps, so the
+        # timed region sees envs as far past their resets (and as often fallen) as the unbudgeted run
+        fin = torch.zeros(n, dtype=torch.int32, device=dev)
+        k0 = 0
+        while k0 < 50 * (a.burn_in + a.warmup) and (k0 % 10 or int(fin.sum()) < n * (a.burn_in + a.warmup)):
+            env.step(acts[k0 % pool])
+            fin += env.ready
+            k0 += 1
+    else:
+        for k in range(k0):
+            env.step(acts[k % pool])
     torch.cuda.synchronize(dev)
     resets0 = sum(h.reset_count() for h in handles)
 
@@ -210,7 +221,7 @@ def main():
     finished = torch.zeros(n, dtype=torch.int32, device=dev) if a.rk_budget else None
     ev0.record(stream)
     for k in range(a.steps):
-        env.step(acts[(a.burn_in + a.warmup + k) % pool])
+        env.step(acts[(k0 + k) % pool])
         if finished is not None:
             finished += env.ready   # envs whose step finished in this launch (one small add per launch)
     ev1.record(stream)
