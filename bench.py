@@ -59,9 +59,10 @@ def host_cores():
     return n
 
 
-def _cpu_rate(env_id, threads, seconds, n_per_thread=64):
+def _cpu_rate(env_id, threads, seconds, n_per_thread=64, integrator='euler'):
     """fp64 C oracle (oracle/, a port of the step): env-steps/s of a batch of
-    n_per_thread x threads envs, auto-reset on the host, bounded sample."""
+    n_per_thread x threads envs, auto-reset on the host, bounded sample;
+    integrator 'euler' (the kernel's default substeps) or 'rk-merson'."""
     import numpy as np
     import oracle
     from bioimitation.registry import load_pack
@@ -71,6 +72,7 @@ def _cpu_rate(env_id, threads, seconds, n_per_thread=64):
     bufs = orc.new_envs(n)
     rng = np.random.Generator(np.random.PCG64(0))
     for i in range(n):
+        orc.set_integrator(bufs, i, integrator, 1e-3)
         orc.reset(bufs, i, int(rng.integers(0, pk.reset_hi + 1)))
     steps, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
@@ -100,6 +102,9 @@ def cpu_baseline(env_id, seconds=12.0):
         if eid != env_id:
             r, s = _cpu_rate(eid, cores, 3.0)
             extra[f'{tag}_{eid[:-3]}'] = {'value': r, 'unit': 'env-steps/s', 'cores': cores, 'sample': s}
+    r, s = _cpu_rate(env_id, cores, 4.0, n_per_thread=16, integrator='rk-merson')
+    extra[f'{env_id[:-3]}_rk_merson'] = {'value': r, 'unit': 'env-steps/s', 'cores': cores, 'sample': s,
+                                         'integrator': 'RK-Merson 1e-3 (the reference integrator)'}
     return {'value': value, 'unit': 'env-steps/s', 'cores': cores, 'kind': 'port',
             'sample': f'{sample}, {env_id}, fp64 C oracle (CPU restatement, not OpenSim), {cores} threads = '
                       f'the CPUs this process may use (affinity, cgroup quota), auto-reset on host',
@@ -143,6 +148,9 @@ def main():
     ap.add_argument('--rk-budget', type=int, default=0,
                     help='rk-merson only: attempts per env per launch (bioim_set_rk_budget); value counts the env '
                          'steps that finished')
+    ap.add_argument('--no-reference-integrator', action='store_true',
+                    help='skip the second measurement: the same workload with the reference integrator '
+                         '(RK-Merson 1e-3, budgeted launches), reported as "reference_integrator"')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--mixed', default=None,
                     help="mixed batch 'ID_A,ID_B' split 50/50 per GPU (BASELINE config C5), e.g. "
@@ -281,10 +289,68 @@ def main():
             line['finished_env_steps'] = steps_total
         if not a.no_cpu_baseline and world == 1:
             line['cpu_baseline'] = cpu_baseline(a.env_id)
-        print(json.dumps(line), flush=True)
     env.close()
+    if not (a.no_reference_integrator or a.mixed or a.integrator != 'semi-implicit'):
+        ref = reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist)
+        if rank == 0:
+            line['reference_integrator'] = ref
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+RK_BUDGET = 6   # attempts per env per launch (DESIGN.md §3 sweep: best at 4096 envs for every ID measured)
+
+
+def reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist):
+    """The same workload (env ID, envs per GPU, actions, auto-reset) with the
+    reference's integrator: RK-Merson at accuracy 1e-3 in budgeted launches
+    (bioim_set_rk_budget; trajectories identical to unbudgeted RK).  Burned in
+    by finished env steps to the same horizon as the main measurement; value =
+    env steps finished in a.steps timed launches over all ranks / max time."""
+    import torch
+    from bioimitation.vector_env import VectorEnv
+    n = a.envs
+    env = VectorEnv(a.env_id, n, config={'integrator': 'rk-merson'}, device=dev.index, precision=a.precision,
+                    seed=1000, auto_reset=True, env_offset=rank * n)
+    env.set_rk_budget(RK_BUDGET)
+    env.reset()
+    fin = torch.zeros(n, dtype=torch.int32, device=dev)
+    k0 = 0
+    while k0 < 50 * (a.burn_in + a.warmup) and (k0 % 10 or int(fin.sum()) < n * (a.burn_in + a.warmup)):
+        env.step(acts[k0 % pool])
+        fin += env.ready
+        k0 += 1
+    resets0 = env.reset_count()
+    fin.zero_()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        env.step(acts[(k0 + k) % pool])
+        fin += env.ready
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    local = int(fin.sum())
+    tot, t_max = float(local), wall
+    if dist:
+        tt = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt[0])
+        st_ = torch.tensor([float(local)], dtype=torch.float64)
+        dist.all_reduce(st_)
+        tot = float(st_[0])
+    rate = {'value': tot / t_max, 'unit': 'finished env-steps/s', 'integrator': 'rk-merson', 'accuracy': 1e-3,
+            'rk_budget': RK_BUDGET, 'launches': a.steps, 'ms_per_launch': t_max / a.steps * 1e3,
+            'finished_env_steps': tot, 'done_rate': (env.reset_count() - resets0) / max(local, 1),
+            'note': "the reference's integrator (opensim_wrapper.py:287-301) on the same workload; "
+                    'GPU parity vs the oracle in tests/test_gpu_parity.py (RK) and tests/test_gpu_rk_budget.py'}
+    env.close()
+    return rate
 
 
 if __name__ == '__main__':
