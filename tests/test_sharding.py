@@ -95,3 +95,16 @@ def test_bench_refuses_mismatched_world_size():
         r = subprocess.run([sys.executable, os.path.join(repo, 'bench.py'), '--gpus', '1', '--no-cpu-baseline'],
                            env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 2 and 'visible' in r.stderr
+
+
+def test_bench_rk_budget_needs_rk_merson():
+    """--rk-budget is an RK-Merson launch mode: asking for it with the default
+    integrator (or a mixed batch) is a usage error, before any GPU work."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for extra in (['--rk-budget', '6'], ['--rk-budget', '6', '--integrator', 'rk-merson', '--mixed', 'A,B']):
+        r = subprocess.run([sys.executable, os.path.join(repo, 'bench.py'), '--no-cpu-baseline'] + extra,
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 2 and '--rk-budget needs' in r.stderr, (extra, r.stderr[-300:])
