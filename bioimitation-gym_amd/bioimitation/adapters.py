@@ -16,6 +16,12 @@ Neither ray nor gym is importable here, so the adapters are duck-typed:
   observation, the terminal one in ``infos['final_observation']``): in-kernel
   auto-reset on.  Outputs are fresh tensors (the env's own buffers are
   overwritten by the next launch), so a replay loop may keep them.
+- :class:`RLlibBaseEnv` — RLlib's asynchronous ``BaseEnv`` protocol (ray
+  1.8, the reference's pin: ``poll`` / ``send_actions`` / ``try_reset``):
+  only the envs that received actions step, and with the reference's
+  RK-Merson integrator in budgeted launches an env whose step is not
+  finished keeps integrating in later launches while the others are polled
+  and sent new actions (``VectorEnv.set_rk_budget``).
 - :class:`MeanStdFilter` — RLlib's ``MeanStdFilter`` (demean, destd,
   clip 10) as a running mean/variance kept on the GPU and updated from whole
   batches, so normalised observations never leave the device.
@@ -179,3 +185,100 @@ class GymVectorEnv:
 
     def close(self):
         self.env.close()
+
+
+class RLlibBaseEnv:
+    """RLlib 1.8 ``BaseEnv`` over one batched HIP env, asynchronous: ``poll()``
+    returns the envs whose step (or reset) finished since the last poll,
+    ``send_actions()`` steps exactly the envs it names (``bioim_set_active_mask``;
+    the others are untouched), ``try_reset()`` resets one env on the device and
+    returns its observation.  With ``config['integrator'] = 'rk-merson'`` the
+    launches are budgeted (``rk_budget`` attempts per env): an
+    env still mid-step after a launch is not polled, ignores new actions and
+    resumes in the next launch, bit-identically, so one stiff env never holds
+    the others.  Dicts are keyed env index -> {``AGENT``: value}; ``dones``
+    carries ``'__all__'`` as RLlib's single-agent wrappers do."""
+
+    AGENT = 'agent0'   # ray.rllib.env.base_env._DUMMY_AGENT_ID (ray 1.8)
+
+    def __init__(self, env_id: str, num_envs: int, config: dict = None, device: int = 0, precision: int = 64,
+                 seed: int = 0, env_offset: int = 0, rk_budget: int = 6):
+        import torch
+        from . import _lib
+        self.env = VectorEnv(env_id, num_envs, config=config, device=device, precision=precision, seed=seed,
+                             auto_reset=False, env_offset=env_offset)
+        self.num_envs = num_envs
+        self.observation_space, self.action_space = _spaces(self.env)
+        self.budgeted = self.env.integrator == 'rk-merson' and rk_budget > 0
+        if self.budgeted:
+            self.env.set_rk_budget(rk_budget)
+        dev = self.env.device
+        self._active = torch.zeros(num_envs, dtype=torch.uint8, device=dev)
+        _lib.check(self.env._L.bioim_set_active_mask(self.env._h, VectorEnv._ptr(self._active)))
+        self._actions = torch.zeros((num_envs, self.env.action_dim), dtype=self.env.dtype, device=dev)
+        self._fresh = np.zeros(num_envs, dtype=bool)      # results not yet polled
+        self._from_reset = np.zeros(num_envs, dtype=bool)
+        self._started = False
+
+    def _rows(self, t, ids):
+        import torch
+        return t[torch.as_tensor(ids, device=self.env.device)].double().cpu().numpy()
+
+    def poll(self):
+        if not self._started:
+            self.env.reset()
+            self._started = True
+            self._fresh[:] = True
+            self._from_reset[:] = True
+        ids = np.nonzero(self._fresh)[0]
+        A = self.AGENT
+        obs, rew, done, info = {}, {}, {}, {}
+        if len(ids):
+            o, r, d, f = (self._rows(t, ids) for t in (self.env.obs, self.env.reward, self.env.done, self.env.info))
+            for k, i in enumerate(ids):
+                i = int(i)
+                obs[i] = {A: o[k]}
+                rew[i] = {A: None if self._from_reset[i] else float(r[k])}
+                dn = False if self._from_reset[i] else bool(d[k])
+                done[i] = {A: dn, '__all__': dn}
+                info[i] = {A: {} if self._from_reset[i] else {'all_rewards': list(map(float, f[k]))}}
+        self._fresh[:] = False
+        self._from_reset[:] = False
+        return obs, rew, done, info, {}
+
+    def send_actions(self, action_dict):
+        import torch
+        ids = [int(i) for i in action_dict]
+        if ids:
+            a = np.stack([np.asarray(action_dict[i][self.AGENT], dtype=np.float64) for i in ids])
+            idx = torch.as_tensor(ids, device=self.env.device)
+            self._actions[idx] = torch.as_tensor(a, dtype=self.env.dtype, device=self.env.device)
+            self._active[idx] = 1
+        for _ in range(1 << 16):    # bounded: a suspended step finishes within its attempt cap
+            if self.budgeted:
+                self.env.ready.zero_()
+            self.env.step(self._actions)
+            ready = (self.env.ready if self.budgeted else self._active).bool().cpu().numpy()
+            self._active.zero_()
+            self._fresh |= ready
+            if ready.any() or not self.budgeted or self.env.pending_count() == 0:
+                break
+
+    def try_reset(self, env_id):
+        i = int(env_id)
+        obs = self.env.reset(env_ids=[i])
+        self._fresh[i] = False
+        return {self.AGENT: obs[i].double().cpu().numpy()}
+
+    def get_sub_environments(self):
+        return []
+
+    get_unwrapped = get_sub_environments
+
+    def try_render(self, env_id=None):
+        return None
+
+    def stop(self):
+        self.env.close()
+
+    close = stop

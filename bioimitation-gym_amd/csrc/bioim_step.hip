@@ -1795,6 +1795,8 @@ template <class T, typename Real> struct LaunchArgs {
     double rk_acc;     /* RK-Merson accuracy (RK kernels) */
     int rk_budget;     /* RK kernels: attempts per env per launch (0: finish every step) */
     uint8_t *ready_out; /* optional [N]: 1 where the env finished its step in this launch */
+    const uint8_t *active; /* optional [N] (steps): 0 = no new action, the env is left untouched
+                              unless it is finishing a suspended RK step */
 };
 
 /* Reference integrator (RK kernels): OpenSim's Manager integrates with an
@@ -1868,6 +1870,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     } else {
         if (gidx >= N) return;
         env = gidx;
+        if (a.active && !a.active[env] && !(RK && st.pend[env] != 0)) return;
     }
     const int H = M.horizon;
     constexpr int MPL = LY::MPL;                  /* muscles / actions per lane: m = lane + j*G */
@@ -2827,6 +2830,7 @@ struct bioim_handle {
     double rk_acc;
     int rk_budget;      /* RK attempts per env per launch, 0: unbudgeted (bioim_set_rk_budget) */
     uint8_t *ready_out; /* caller's device buffer [n] or null */
+    const uint8_t *active; /* caller's device buffer [n] or null (bioim_set_active_mask) */
     Ops ops;
     bioim_modelpack_t pack;
 };
@@ -2866,6 +2870,7 @@ LaunchArgs<T, Real> make_args(bioim_handle_t *h, int mode, const void *actions, 
     a.rk_acc = h->rk_acc;
     a.rk_budget = h->rk ? h->rk_budget : 0;
     a.ready_out = mode == 0 ? h->ready_out : nullptr;
+    a.active = mode == 0 ? h->active : nullptr;
     return a;
 }
 
@@ -3167,6 +3172,12 @@ int bioim_set_rk_budget(bioim_handle_t *h, int attempts, uint8_t *ready_out) {
     if (!h || attempts < 0) return fail(BIOIM_E_ARG, "bioim_set_rk_budget: null handle or negative budget");
     h->rk_budget = attempts;
     h->ready_out = ready_out;
+    return 0;
+}
+
+int bioim_set_active_mask(bioim_handle_t *h, const uint8_t *active) {
+    if (!h) return fail(BIOIM_E_ARG, "null handle");
+    h->active = active;
     return 0;
 }
 

@@ -162,6 +162,11 @@ int bioim_set_integrator(bioim_handle_t *h, int kind, double accuracy);
 int bioim_set_rk_budget(bioim_handle_t *h, int attempts, uint8_t *ready_out);
 /* envs suspended mid-step (synchronizes the handle's stream) */
 int bioim_pending_count(bioim_handle_t *h);
+/* Optional per-env step mask (device [n], NULL = every env steps): an env
+ * with 0 is left untouched by bioim_step (state, outputs, ready flag) unless
+ * it is finishing a suspended RK step.  Lets an asynchronous consumer step
+ * only the envs it sent actions to (RLlib BaseEnv.send_actions). */
+int bioim_set_active_mask(bioim_handle_t *h, const uint8_t *active);
 /* Optional terminal-observation output: when set (a device buffer with the
  * handle's obs row stride), every step also writes each env's observation
  * as computed by that step *before* an in-kernel auto-reset replaces it, so

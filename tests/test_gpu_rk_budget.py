@@ -94,3 +94,58 @@ def test_rk_budget_state_roundtrip_clears_pending():
     env.set_state(s)
     assert env.pending_count() == 0
     env.close()
+
+
+def _sync_reference(env_id, n, T, acts, integrator, seed):
+    import torch
+    from bioimitation.vector_env import VectorEnv
+    env = VectorEnv(env_id, n, config={'integrator': integrator}, precision=64, seed=seed)
+    o0 = env.reset().cpu().numpy().copy()
+    out = []
+    for k in range(T):
+        o, r, d, _ = env.step(torch.as_tensor(acts[k], device=env.device))
+        out.append((o.cpu().numpy().copy(), r.cpu().numpy().copy(), d.cpu().numpy().copy()))
+    env.close()
+    return o0, out
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs a HIP GPU')
+@pytest.mark.parametrize('integrator,env_id', [('rk-merson', 'MuscleRunningImitation3D-v0'),
+                                               ('semi-implicit', 'MuscleWalkingImitation2D-v0')])
+def test_rllib_base_env_async_equals_sync(integrator, env_id):
+    """RLlibBaseEnv driven like RLlib 1.8's sampler (poll, then actions for the
+    polled envs only): each env follows its own action sequence and its
+    results equal a synchronous run's bit for bit.  Semi-implicit: the runner
+    withholds actions from every third env at every other round, so the
+    active mask must leave those envs untouched."""
+    from bioimitation.adapters import RLlibBaseEnv
+    from bioimitation.registry import load_pack
+    pk = load_pack(env_id)
+    n, T, seed = 48, 10, 3
+    rng = np.random.default_rng(11)
+    acts = rng.uniform(0, 0.5, size=(T, n, pk.nact))
+    o0, ref = _sync_reference(env_id, n, T, acts, integrator, seed)
+    benv = RLlibBaseEnv(env_id, n, config={'integrator': integrator}, seed=seed, rk_budget=5)
+    obs, rew, done, info, _ = benv.poll()
+    assert sorted(obs) == list(range(n)) and all(rew[i][benv.AGENT] is None for i in range(n))
+    np.testing.assert_array_equal(np.stack([obs[i][benv.AGENT] for i in range(n)]), o0)
+    k = np.zeros(n, dtype=int)
+    waiting = set(range(n))          # polled, not yet sent an action
+    rounds = 0
+    while k.min() < T and rounds < 60 * T:
+        rounds += 1
+        send = {i: {benv.AGENT: acts[k[i]][i]} for i in sorted(waiting) if k[i] < T and
+                not (integrator == 'semi-implicit' and i % 3 == 0 and rounds % 2 == 0)}
+        waiting -= set(send)
+        benv.send_actions(send)
+        obs, rew, done, info, _ = benv.poll()
+        for i, ob in obs.items():
+            assert i in send or integrator == 'rk-merson', f'env {i} polled without having been sent an action'
+            t = k[i]
+            np.testing.assert_array_equal(ob[benv.AGENT], ref[t][0][i], err_msg=f'obs env {i} step {t}')
+            assert rew[i][benv.AGENT] == ref[t][1][i] and done[i][benv.AGENT] == bool(ref[t][2][i]), (i, t)
+            k[i] += 1
+            waiting.add(i)
+    print(f'{env_id} ({integrator}): {rounds} rounds for {T} steps per env')
+    assert (k >= T).all(), k
+    benv.stop()
