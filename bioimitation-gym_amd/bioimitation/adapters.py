@@ -204,7 +204,6 @@ class RLlibBaseEnv:
     def __init__(self, env_id: str, num_envs: int, config: dict = None, device: int = 0, precision: int = 64,
                  seed: int = 0, env_offset: int = 0, rk_budget: int = 6):
         import torch
-        from . import _lib
         self.env = VectorEnv(env_id, num_envs, config=config, device=device, precision=precision, seed=seed,
                              auto_reset=False, env_offset=env_offset)
         self.num_envs = num_envs
@@ -214,7 +213,7 @@ class RLlibBaseEnv:
             self.env.set_rk_budget(rk_budget)
         dev = self.env.device
         self._active = torch.zeros(num_envs, dtype=torch.uint8, device=dev)
-        _lib.check(self.env._L.bioim_set_active_mask(self.env._h, VectorEnv._ptr(self._active)))
+        self.env.set_active_mask(self._active)
         self._actions = torch.zeros((num_envs, self.env.action_dim), dtype=self.env.dtype, device=dev)
         self._fresh = np.zeros(num_envs, dtype=bool)      # results not yet polled
         self._from_reset = np.zeros(num_envs, dtype=bool)

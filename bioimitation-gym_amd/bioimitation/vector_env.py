@@ -146,6 +146,14 @@ class VectorEnv:
             self.ready = None
         _lib.check(self._L.bioim_set_rk_budget(self._h, self.rk_budget, self._ptr(self.ready)))
 
+    def set_active_mask(self, mask):
+        """Per-env step mask (``bioim_set_active_mask``): a (N,) uint8 device
+        tensor read by every later ``step()``; envs with 0 are left untouched
+        unless they are finishing a suspended RK step.  ``None`` steps all.
+        The tensor must stay alive while it is set."""
+        self._active = mask
+        _lib.check(self._L.bioim_set_active_mask(self._h, self._ptr(mask)))
+
     def pending_count(self) -> int:
         """Envs suspended mid-step by the RK budget."""
         return _lib.check(self._L.bioim_pending_count(self._h))
