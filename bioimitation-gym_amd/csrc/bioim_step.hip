@@ -391,38 +391,6 @@ template <class T> DEV int mslot(int s) {
     return r;
 }
 
-/* composite bodies carrying contact spheres (the feet), in first-appearance
- * order of T::sphere_cb */
-template <class T> struct Feet {
-    static constexpr int count() {
-        int n = 0;
-        for (int s = 0; s < T::NS; ++s) {
-            bool seen = false;
-            for (int r = 0; r < s; ++r) seen = seen || T::sphere_cb[r] == T::sphere_cb[s];
-            n += seen ? 0 : 1;
-        }
-        return n;
-    }
-    static constexpr int N = count();
-    static constexpr int cb(int i) {   /* composite body of foot i */
-        int n = 0;
-        for (int s = 0; s < T::NS; ++s) {
-            bool seen = false;
-            for (int r = 0; r < s; ++r) seen = seen || T::sphere_cb[r] == T::sphere_cb[s];
-            if (!seen) {
-                if (n == i) return T::sphere_cb[s];
-                ++n;
-            }
-        }
-        return -1;
-    }
-    static constexpr int of(int sp) {  /* foot index of sphere sp */
-        for (int i = 0; i < N; ++i)
-            if (cb(i) == T::sphere_cb[sp]) return i;
-        return 0;
-    }
-};
-
 /* ---------------------------------------------------------- LDS layout
  * Per workgroup: the shared model image (SModel, bioim_device.h), then one
  * region per env.  Phase 1 (lane-parallel kinematics) publishes frames,
@@ -434,7 +402,6 @@ template <class T, typename Real> struct Lay {
     static constexpr int NB = T::NB, ND = T::ND > 0 ? T::ND : 1, NC = T::NC, NP = ND * (ND + 1) / 2;
     static constexpr int NMS = T::NM > T::NA ? T::NM : T::NA;
     static constexpr int MPL = (NMS + T::G - 1) / T::G;      /* muscles (actions) per lane            */
-    static constexpr int NTL = NMS < T::G ? NMS : T::G;      /* lanes holding muscles / actuators     */
     static constexpr int NS = T::NS > 0 ? T::NS : 1, NL = T::NL > 0 ? T::NL : 1;
     static constexpr int CJN = 10;               /* per sphere: P3, F3 (implicit), C4 (xx xz yy zz)  */
     static constexpr int NTR = (T::TX >= 0) + (T::TY >= 0) + (T::TZ >= 0);
@@ -458,18 +425,14 @@ template <class T, typename Real> struct Lay {
     static constexpr int LOC = U;                /* phase 1: [NB+1][24] joint-local data (NB: identity) */
     static constexpr int SL = LOC + 24 * (NB + 1); /* phase 1: [ND][6] joint-local Plucker columns  */
     /* phases 2-3: [MPL * G][MAXSPAN] per muscle slot, -F_t dL/dq over its
-     * span (actuator slot: its torque), then one zero slot (TZ); at least
-     * NTL * ND reals (the region is shared with the phase-3 vectors) */
+     * span (actuator slot: its torque), then one zero slot (TZ) */
     static constexpr int TZ = MPL * T::G * T::MAXSPAN;
-    static constexpr int TAUN = TZ + 1 > NTL * ND ? TZ + 1 : NTL * ND;
+    static constexpr int TAUN = TZ + 1;
     static constexpr int TAU = U;
     static constexpr int CJ = TAU + TAUN;        /* phases 2-3: [NS][CJN] contact slots             */
     static constexpr int OBS = U;                /* report: observation staging                     */
     static constexpr int REP = OBS + OBSMAX;     /* report: [NOS+1][6] body pos/vel (NOS: COM)      */
-    static constexpr int NFB = Feet<T>::N;       /* feet: phase-3 implicit contact vectors [NFB][ND][6] at TAU */
-    static constexpr int FD = 6 * NFB * ND;      /* phase 3: [ND][6] I^c S_d (after Y, relative to TAU)     */
-    static constexpr int U2A = TAUN + NS * CJN, U2B = 6 * (NFB + 1) * ND;
-    static constexpr int U1 = 24 * (NB + 1) + 6 * ND, U2 = U2A > U2B ? U2A : U2B;
+    static constexpr int U1 = 24 * (NB + 1) + 6 * ND, U2 = TAUN + NS * CJN;
     static constexpr int U3 = OBSMAX + 6 * (T::NOS + 1);
     static constexpr int USZ = U1 > U2 ? (U1 > U3 ? U1 : U3) : (U2 > U3 ? U2 : U3);
     static constexpr int SIZE = ((U + USZ + 1) / 2) * 2;
@@ -862,6 +825,13 @@ template <class T> struct DofTree {
         for (int j = par(k); j >= 0; j = par(j))
             if (j == i) return true;
         return false;
+    }
+    /* bit l set: l is k or an ancestor dof of k (the structurally non-zero
+     * entries (k, l) of row k of M) */
+    static constexpr unsigned path_mask(int k) {
+        unsigned m = 1u << k;
+        for (int j = par(k); j >= 0; j = par(j)) m |= 1u << j;
+        return m;
     }
 };
 
@@ -1392,26 +1362,37 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     wave_sync();
     STAMP(7);
 
-    /* ---- phase 3: right-hand side and mass-matrix entries, fixed-order sums.
-     * 3a (lane = dof d): rhs_d = -S_d.WB + muscle/actuator torques + contact
-     * J_d(s).F_s + limits; for the implicit step also the per-foot vectors
-     * Y_{b,d} = sum_{s on b} (P_s x w, w), w = C_s J_d(s), so that the
-     * implicit contact block of an entry is sum_b S_l . Y_{b,k} (six FMAs per
-     * foot instead of a Jacobian pair and a 3x3 form per sphere).
-     * 3b: Y to LDS (over the consumed torque slots).  3c (lane = entry):
-     * composite-rigid-body M entries + implicit contact and limit terms. */
-    using FT = Feet<T>;
+    /* ---- phase 3 (lane = dof k): right-hand side and row k of the packed
+     * lower M, fixed-order sums.
+     * rhs_k = -S_k.WB + muscle/actuator torques + contact J_k(s).F_s + limits.
+     * Row k holds the entries (k, l) for the dofs l on k's root path (l = k
+     * included; the others are structural zeros, never read by ltl_solve):
+     * M_kl = S_l . I^c S_k, the composite inertia of k's body times k's
+     * column (CRBA).  The implicit contact block of an entry is
+     * J_l(s)^T C_s J_k(s) over the spheres s below k; with
+     * J_l(s)^T w = S_l . (P_s x w, w) it folds into the same vector:
+     * G_k = I^c S_k + sum_s (P_s x w_s, w_s), w_s = C_s J_k(s), and
+     * M_kl = S_l . G_k (every l on k's path moves the spheres k moves).  All
+     * inputs (S, IC, CJ, LIM) were published before the last sync, so the
+     * row needs no exchange between lanes. */
     const bool implicit = h > 0;
     if (lane < ND) {
         const Real *Sd = lds + LY::S + 6 * lane, *wb = lds + LY::WB + 6 * SM.dof_cb[lane];
         Real r = -(dot3(Sd, wb) + dot3(Sd + 3, wb + 3));
 #pragma unroll
         for (int i = 0; i < T::MAXARM; ++i) r += lds[LY::TAU + SM.tau_src[lane][i]];
-        Real Y[FT::N > 0 ? FT::N : 1][6];
+        Real Gk[6];
+        {
+            const Real *ic = lds + LY::IC + 10 * SM.dof_cb[lane];
+            Real t[3];
+            symv(ic + 4, Sd, Gk);
+            cross3(ic + 1, Sd + 3, t);
 #pragma unroll
-        for (int b = 0; b < FT::N; ++b)
+            for (int i = 0; i < 3; ++i) Gk[i] += t[i];
+            cross3(Sd, ic + 1, t);
 #pragma unroll
-            for (int i = 0; i < 6; ++i) Y[b][i] = 0;
+            for (int i = 0; i < 3; ++i) Gk[3 + i] = ic[0] * Sd[3 + i] + t[i];
+        }
         sfor<0, T::NS>([&](auto sI) {
             constexpr int sp = decltype(sI)::value;
             constexpr unsigned msk = T::dofmask[T::sphere_cb[sp]];
@@ -1424,73 +1405,36 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
                 Real w[3] = {C[0] * jd[0] + C[1] * jd[2], C[2] * jd[1], C[1] * jd[0] + C[3] * jd[2]};
                 Real pw[3];
                 cross3(cj, w, pw);
-                constexpr int fb = FT::of(sp);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
-                    Y[fb][i] += on ? pw[i] : Real(0);
-                    Y[fb][3 + i] += on ? w[i] : Real(0);
+                    Gk[i] += on ? pw[i] : Real(0);
+                    Gk[3 + i] += on ? w[i] : Real(0);
                 }
             }
         });
+        Real dg = 0;
 #pragma unroll
         for (int li = 0; li < T::NL; ++li)
-            if (SM.lim_dof[li] == lane) r += lds[LY::LIM + 4 * li + 2];
+            if (SM.lim_dof[li] == lane) { r += lds[LY::LIM + 4 * li + 2]; dg += lds[LY::LIM + 4 * li + 1]; }
         lds[LY::RHS + lane] = r;
-        /* F_d = I^c S_d, the composite inertia of dof d's body times its
-         * column: entry (l, k) of M is S_other . F_deeper */
-        Real Fd[6];
-        {
-            const Real *ic = lds + LY::IC + 10 * SM.dof_cb[lane];
-            Real t[3];
-            symv(ic + 4, Sd, Fd);
-            cross3(ic + 1, Sd + 3, t);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) Fd[i] += t[i];
-            cross3(Sd, ic + 1, t);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) Fd[3 + i] = ic[0] * Sd[3 + i] + t[i];
-        }
-        wave_sync_lanes();   /* every dof lane has read the torque and contact slots */
-#pragma unroll
-        for (int i = 0; i < 6; ++i) lds[LY::TAU + LY::FD + 6 * lane + i] = Fd[i];
-        if (implicit) {
-#pragma unroll
-            for (int b = 0; b < FT::N; ++b)
-#pragma unroll
-                for (int i = 0; i < 6; ++i) lds[LY::TAU + 6 * (ND * b + lane) + i] = Y[b][i];
-        }
-    }
-    wave_sync();
-    auto m_entry = [&](int e) {
-        const uint32_t ep = SM.e_pk[e];
-        const int l = ep & 0xff, k = (ep >> 8) & 0xff, dp = (ep >> 16) & 0xff, ot = ep >> 24;
-        const Real *Sl = lds + LY::S + 6 * l;
-        Real v = 0;
-        if (dp != 0xff) {
-            const Real *So = lds + LY::S + 6 * ot, *Fp = lds + LY::TAU + LY::FD + 6 * dp;
-            v = dot3(So, Fp) + dot3(So + 3, Fp + 3);
-        }
-        if (implicit) {
-            /* implicit contact: S_l . Y_{b,k} for each foot b both dofs move */
-#pragma unroll
-            for (int b = 0; b < FT::N; ++b) {
-                const unsigned msk = T::dofmask[FT::cb(b)];
-                const Real *y = lds + LY::TAU + 6 * (ND * b + k);
-                const Real term = dot3(Sl, y) + dot3(Sl + 3, y + 3);
-                v += ((msk >> l) & (msk >> k) & 1u) ? term : Real(0);
+        /* dofs on k's root path, k included (compile-time per dof, selected by lane) */
+        unsigned path = 0;
+        sfor<0, ND>([&](auto kI) {
+            constexpr int k = decltype(kI)::value;
+            constexpr unsigned pm = DofTree<T>::path_mask(k);
+            path = lane == k ? pm : path;
+        });
+        Real *row = lds + LY::MP + (lane * (lane + 1)) / 2;
+        sfor<0, ND>([&](auto lI) {
+            constexpr int l = decltype(lI)::value;
+            if ((path >> l) & 1u) {
+                const Real *Sl = lds + LY::S + 6 * l;
+                Real v = dot3(Sl, Gk) + dot3(Sl + 3, Gk + 3);
+                if (implicit && l == lane) v += dg;
+                row[l] = v;
             }
-            if (l == k)
-#pragma unroll
-                for (int li = 0; li < T::NL; ++li)
-                    if (SM.lim_dof[li] == l) v += lds[LY::LIM + 4 * li + 1];
-        }
-        lds[LY::MP + e] = v;
-    };
-    /* all passes over the entries unrolled: their LDS loads can be issued
-     * ahead of the previous pass's FMAs */
-#pragma unroll
-    for (int pass = 0; pass < (NP + G - 1) / G; ++pass)
-        if ((pass + 1) * G <= NP || lane + pass * G < NP) m_entry(lane + pass * G);
+        });
+    }
     wave_sync();
     STAMP(8);
 
