@@ -95,6 +95,87 @@ template <typename Real> DEV void mm3(const Real *A, const Real *B, Real *C) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) C[i] = T[i];
 }
+/* The same products with compile-time zero masks (bit i: operand entry i
+ * is known to be zero): a term with a known-zero factor is left out, so
+ * planar models (Planar below) run the 2-D arithmetic through the same
+ * code; with empty masks these are exactly mv3 / mm3 / cross3 / dot3
+ * (same terms, same order). */
+template <unsigned ZA, unsigned ZB, int N, typename Real>
+DEV Real sum_m(const Real *a, const Real *b, const int (&ia)[N], const int (&ib)[N], const int (&sg)[N]) {
+    Real acc = 0;
+    bool first = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        if (((ZA >> ia[k]) & 1u) || ((ZB >> ib[k]) & 1u)) continue;
+        const Real t = a[ia[k]] * b[ib[k]];
+        acc = first ? (sg[k] > 0 ? t : -t) : (sg[k] > 0 ? acc + t : acc - t);
+        first = false;
+    }
+    return acc;
+}
+template <unsigned ZA, unsigned ZB, typename Real> DEV void mv3m(const Real *R, const Real *v, Real *o) {
+    Real r[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int ia[3] = {3 * i, 3 * i + 1, 3 * i + 2}, ib[3] = {0, 1, 2}, sg[3] = {1, 1, 1};
+        r[i] = sum_m<ZA, ZB, 3>(R, v, ia, ib, sg);
+    }
+    o[0] = r[0]; o[1] = r[1]; o[2] = r[2];
+}
+template <unsigned ZA, unsigned ZB, typename Real> DEV void mm3m(const Real *A, const Real *B, Real *C) {
+    Real T[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int ia[3] = {3 * i, 3 * i + 1, 3 * i + 2}, ib[3] = {j, 3 + j, 6 + j}, sg[3] = {1, 1, 1};
+            T[3 * i + j] = sum_m<ZA, ZB, 3>(A, B, ia, ib, sg);
+        }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) C[i] = T[i];
+}
+template <unsigned ZA, unsigned ZB, typename Real> DEV void cross3m(const Real *a, const Real *b, Real *o) {
+    const int sg[2] = {1, -1};
+    const int ia0[2] = {1, 2}, ib0[2] = {2, 1}, ia1[2] = {2, 0}, ib1[2] = {0, 2}, ia2[2] = {0, 1}, ib2[2] = {1, 0};
+    Real x = sum_m<ZA, ZB, 2>(a, b, ia0, ib0, sg), y = sum_m<ZA, ZB, 2>(a, b, ia1, ib1, sg),
+         z = sum_m<ZA, ZB, 2>(a, b, ia2, ib2, sg);
+    o[0] = x; o[1] = y; o[2] = z;
+}
+template <unsigned ZA, unsigned ZB, typename Real> DEV Real dot3m(const Real *a, const Real *b) {
+    const int ia[3] = {0, 1, 2}, sg[3] = {1, 1, 1};
+    return sum_m<ZA, ZB, 3>(a, b, ia, ia, sg);
+}
+
+/* Planar topologies (T::PLANAR; the host checks each pack, pack_is_planar):
+ * frames rotate about z only, so R13 = R23 = R31 = R32 = 0 and R33 = 1,
+ * angular velocities and accelerations lie along z, linear ones in the x-y
+ * plane.  These helpers write those zeros over values just read from LDS;
+ * in the functions that use them the products with the known zeros then fold
+ * away (those functions are compiled without signed zeros / NaN semantics:
+ * `#pragma float_control(precise, off)`), so a planar model runs 2-D
+ * arithmetic through the same source.  No-ops for spatial topologies. */
+template <class T> struct Planar {
+    /* zero masks (mv3m / mm3m / cross3m / dot3m): rotation, angular, linear */
+    static constexpr unsigned ZR = T::PLANAR ? 0xE4u : 0u, ZW = T::PLANAR ? 0x3u : 0u, ZV = T::PLANAR ? 0x4u : 0u;
+    template <typename Real> static DEV void rot(Real *R) {
+        if constexpr (T::PLANAR) { R[2] = R[5] = R[6] = R[7] = Real(0); R[8] = Real(1); }
+    }
+    template <typename Real> static DEV void ang(Real *w) {
+        if constexpr (T::PLANAR) { w[0] = w[1] = Real(0); }
+    }
+    template <typename Real> static DEV void lin(Real *v) {
+        if constexpr (T::PLANAR) { v[2] = Real(0); }
+    }
+    /* frame slot KB: R9 o3 w3 vO3 */
+    template <typename Real> static DEV void frame(Real *kb) { rot(kb); ang(kb + 12); lin(kb + 15); }
+    /* joint-local slot LOC: R9 p3 wrel3 vrel3 arel3 aa3 */
+    template <typename Real> static DEV void loc(Real *lc) { rot(lc); ang(lc + 12); lin(lc + 15); ang(lc + 18); lin(lc + 21); }
+    /* acceleration slot AL: alpha3 aO3 */
+    template <typename Real> static DEV void acc(Real *ab) { ang(ab); lin(ab + 3); }
+    /* Plucker column: Omega3 V3 */
+    template <typename Real> static DEV void col(Real *s) { ang(s); lin(s + 3); }
+};
+
 DEV void sincos_rt(double x, double &s, double &c);
 DEV void sincos_rt(float x, float &s, float &c);
 template <typename Real> DEV void axis_rot(const Real *a, Real th, Real *R) {
@@ -500,6 +581,8 @@ DEV void publish_coords(const DModel<Real> &M, const SModel<T, Real> &SM, Real *
 template <class T, typename Real>
 DEV void kin_local(const SModel<T, Real> &SM, Real *lds, int c) {
     using LY = Lay<T, Real>;
+    using PL = Planar<T>;
+    constexpr unsigned ZR = PL::ZR, ZW = PL::ZW, ZV = PL::ZV;
     constexpr unsigned USED = TopoInfo<T>::axes_used();
     const SBody<Real> &b = SM.body[c];
     Real RFM[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
@@ -529,64 +612,72 @@ DEV void kin_local(const SModel<T, Real> &SM, Real *lds, int c) {
             cd[ax] = cc >= 0 ? SM.coord_dof[cs] : -1;
             Real a[3] = {b.axis[ax][0], b.axis[ax][1], b.axis[ax][2]};
             if constexpr (ax < 3) {
+                PL::ang(a);
                 Real ucol[3], cr[3];
-                mv3(RFM, a, ucol);
+                mv3m<ZR, ZW>(RFM, a, ucol);
                 Real thd = f1 * uc;
-                cross3(wrel, ucol, cr);
+                cross3m<ZW, ZW>(wrel, ucol, cr);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
                     arel[i] += ucol[i] * (f2 * uc * uc) + cr[i] * thd;
                     wrel[i] += ucol[i] * thd;
                     col[ax][i] = ucol[i] * f1;
                 }
+                PL::ang(arel); PL::ang(wrel); PL::ang(col[ax]);
                 Real Rk[9];
                 axis_rot(a, f, Rk);  /* f == 0 (absent axis): identity */
-                mm3(RFM, Rk, RFM);
+                PL::rot(Rk);
+                mm3m<ZR, ZR>(RFM, Rk, RFM);
             } else {
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
                     pFM[i] += a[i] * f; pd[i] += a[i] * (f1 * uc); pdd[i] += a[i] * (f2 * uc * uc);
                     col[ax][i] = a[i] * f1;
                 }
+                PL::lin(pd); PL::lin(pdd); PL::lin(col[ax]);
             }
         }
     });
+    Real Rpf[9], Rmb[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) { Rpf[i] = b.R_pf[i]; Rmb[i] = b.R_mb[i]; }
+    PL::rot(Rpf); PL::rot(Rmb);
     Real dF[3], T9[9], RPB[9], pm[3], pPB[3];
-    mv3(RFM, b.p_mb, dF);
-    mm3(b.R_pf, RFM, T9);
-    mm3(T9, b.R_mb, RPB);
+    mv3m<ZR, 0>(RFM, b.p_mb, dF);
+    mm3m<ZR, ZR>(Rpf, RFM, T9);
+    mm3m<ZR, ZR>(T9, Rmb, RPB);
 #pragma unroll
     for (int i = 0; i < 3; ++i) pm[i] = pFM[i] + dF[i];
-    mv3(b.R_pf, pm, pPB);
+    mv3m<ZR, 0>(Rpf, pm, pPB);
     Real *lc = lds + LY::LOC + 24 * c;
 #pragma unroll
     for (int i = 0; i < 9; ++i) lc[i] = RPB[i];
 #pragma unroll
     for (int i = 0; i < 3; ++i) lc[9 + i] = pPB[i] + b.p_pf[i];
     Real t1[3], t2[3], t3[3], o[3];
-    mv3(b.R_pf, wrel, o);
+    mv3m<ZR, ZW>(Rpf, wrel, o);
 #pragma unroll
     for (int i = 0; i < 3; ++i) lc[12 + i] = o[i];
-    cross3(wrel, dF, t1);
+    cross3m<ZW, 0>(wrel, dF, t1);
 #pragma unroll
     for (int i = 0; i < 3; ++i) t2[i] = pd[i] + t1[i];
-    mv3(b.R_pf, t2, o);
+    mv3m<ZR, ZV>(Rpf, t2, o);
 #pragma unroll
     for (int i = 0; i < 3; ++i) lc[15 + i] = o[i];
-    mv3(b.R_pf, arel, o);
+    mv3m<ZR, ZW>(Rpf, arel, o);
 #pragma unroll
     for (int i = 0; i < 3; ++i) lc[18 + i] = o[i];
-    cross3(arel, dF, t2);
-    cross3(wrel, t1, t3);
+    cross3m<ZW, 0>(arel, dF, t2);
+    cross3m<ZW, ZV>(wrel, t1, t3);
 #pragma unroll
     for (int i = 0; i < 3; ++i) t2[i] = pdd[i] + t2[i] + t3[i];
-    mv3(b.R_pf, t2, o);
+    mv3m<ZR, ZV>(Rpf, t2, o);
 #pragma unroll
     for (int i = 0; i < 3; ++i) lc[21 + i] = o[i];
     /* Plucker columns in the parent frame, linear part at the parent origin;
      * rotations act about the M origin pM = p_pf + R_pf pFM */
     Real pM[3];
-    mv3(b.R_pf, pFM, pM);
+    mv3m<ZR, 0>(Rpf, pFM, pM);
 #pragma unroll
     for (int i = 0; i < 3; ++i) pM[i] += b.p_pf[i];
     sfor<0, 6>([&](auto aI) {
@@ -595,15 +686,20 @@ DEV void kin_local(const SModel<T, Real> &SM, Real *lds, int c) {
             if (cd[ax] >= 0) {
                 Real *sl = lds + LY::SL + 6 * cd[ax];
                 Real v[3];
-                mv3(b.R_pf, col[ax], v);
                 if constexpr (ax < 3) {
+                    mv3m<ZR, ZW>(Rpf, col[ax], v);
                     Real lin[3];
-                    cross3(pM, v, lin);
+                    cross3m<0, ZW>(pM, v, lin);
 #pragma unroll
-                    for (int i = 0; i < 3; ++i) { sl[i] += v[i]; sl[3 + i] += lin[i]; }
+                    for (int i = 0; i < 3; ++i) {
+                        if (!((ZW >> i) & 1u)) sl[i] += v[i];
+                        if (!((ZV >> i) & 1u)) sl[3 + i] += lin[i];
+                    }
                 } else {
+                    mv3m<ZR, ZV>(Rpf, col[ax], v);
 #pragma unroll
-                    for (int i = 0; i < 3; ++i) sl[3 + i] += v[i];
+                    for (int i = 0; i < 3; ++i)
+                        if (!((ZV >> i) & 1u)) sl[3 + i] += v[i];
                 }
             }
         }
@@ -617,42 +713,45 @@ template <typename Real> struct Frame {
     Real R[9], o[3], w[3], vO[3], al[3], aO[3];
 };
 
-/* F := F composed with the joint whose parent-frame data is lc (LOC slot) */
-template <typename Real> DEV void compose(Frame<Real> &F, const Real *lc) {
+/* F := F composed with the joint whose parent-frame data is lc (LOC slot).
+ * Zero masks: R rotations, w/wrg/al angular, vO/vrel/aO/aa linear (Planar) */
+template <class T, typename Real> DEV void compose(Frame<Real> &F, const Real *lc) {
+    using PL = Planar<T>;
+    constexpr unsigned ZR = PL::ZR, ZW = PL::ZW, ZV = PL::ZV;
     Real R[9], oB[3], w[3], wrg[3], vrel[3], vO[3], al[3], t[3], t2[3], t3[3];
-    mm3(F.R, lc, R);
-    mv3(F.R, lc + 9, t);
+    mm3m<ZR, ZR>(F.R, lc, R);
+    mv3m<ZR, 0>(F.R, lc + 9, t);
 #pragma unroll
     for (int i = 0; i < 3; ++i) oB[i] = F.o[i] + t[i];
-    mv3(F.R, lc + 12, wrg);
+    mv3m<ZR, ZW>(F.R, lc + 12, wrg);
 #pragma unroll
     for (int i = 0; i < 3; ++i) w[i] = F.w[i] + wrg[i];
-    mv3(F.R, lc + 15, vrel);
-    cross3(wrg, oB, t);
+    mv3m<ZR, ZV>(F.R, lc + 15, vrel);
+    cross3m<ZW, 0>(wrg, oB, t);
 #pragma unroll
     for (int i = 0; i < 3; ++i) vO[i] = F.vO[i] + vrel[i] - t[i];
-    mv3(F.R, lc + 18, t);
-    cross3(F.w, wrg, t2);
+    mv3m<ZR, ZW>(F.R, lc + 18, t);
+    cross3m<ZW, ZW>(F.w, wrg, t2);
 #pragma unroll
     for (int i = 0; i < 3; ++i) al[i] = F.al[i] + t2[i] + t[i];
     /* acceleration of the new origin: parent point acceleration
      * + Coriolis 2 wP x vrel + relative acceleration */
     Real vpt[3], aB[3], aa[3];
-    cross3(F.w, oB, t);
+    cross3m<ZW, 0>(F.w, oB, t);
 #pragma unroll
     for (int i = 0; i < 3; ++i) vpt[i] = F.vO[i] + t[i];
-    cross3(F.al, oB, t);
-    cross3(F.w, vpt, t2);
-    cross3(F.w, vrel, t3);
-    mv3(F.R, lc + 21, aa);
+    cross3m<ZW, 0>(F.al, oB, t);
+    cross3m<ZW, ZV>(F.w, vpt, t2);
+    cross3m<ZW, ZV>(F.w, vrel, t3);
+    mv3m<ZR, ZV>(F.R, lc + 21, aa);
 #pragma unroll
     for (int i = 0; i < 3; ++i) aB[i] = F.aO[i] + t[i] + t2[i] + Real(2) * t3[i] + aa[i];
     Real vB[3];
-    cross3(w, oB, t);
+    cross3m<ZW, 0>(w, oB, t);
 #pragma unroll
     for (int i = 0; i < 3; ++i) vB[i] = vO[i] + t[i];
-    cross3(al, oB, t);
-    cross3(w, vB, t2);
+    cross3m<ZW, 0>(al, oB, t);
+    cross3m<ZW, ZV>(w, vB, t2);
 #pragma unroll
     for (int i = 0; i < 9; ++i) F.R[i] = R[i];
 #pragma unroll
@@ -660,6 +759,7 @@ template <typename Real> DEV void compose(Frame<Real> &F, const Real *lc) {
         F.aO[i] = aB[i] - t[i] - t2[i];
         F.o[i] = oB[i]; F.w[i] = w[i]; F.vO[i] = vO[i]; F.al[i] = al[i];
     }
+    PL::rot(F.R); PL::ang(F.w); PL::lin(F.vO); PL::ang(F.al); PL::lin(F.aO);
 }
 
 /* identity joint (LOC slot NB) and the ground frame (KB/AL slot NB) */
@@ -688,7 +788,12 @@ DEV void kin_chain(const SModel<T, Real> &SM, Real *lds, int c, Real x0) {
     for (int i = 0; i < 3; ++i) { F.o[i] = i == 0 ? -x0 : Real(0); F.w[i] = 0; F.vO[i] = 0; F.al[i] = 0; F.aO[i] = 0; }
     sfor<0, TopoInfo<T>::depth()>([&](auto lI) {
         constexpr int lvl = decltype(lI)::value;
-        compose(F, lds + LY::LOC + 24 * SM.chain[c][lvl]);
+        const Real *src = lds + LY::LOC + 24 * SM.chain[c][lvl];
+        Real lc[24];
+#pragma unroll
+        for (int i = 0; i < 24; ++i) lc[i] = src[i];
+        Planar<T>::loc(lc);
+        compose<T, Real>(F, lc);
     });
     Real *kb = lds + LY::KB + 18 * c, *ab = lds + LY::AL + 6 * c;
 #pragma unroll
@@ -722,12 +827,20 @@ DEV void fn_slots(const SModel<T, Real> &SM, Real *lds, int lane) {
 template <class T, typename Real>
 DEV void kin_column(const SModel<T, Real> &SM, Real *lds, int d) {
     using LY = Lay<T, Real>;
+    using PL = Planar<T>;
+    constexpr unsigned ZR = PL::ZR, ZW = PL::ZW, ZV = PL::ZV;
     const Real *kp = lds + LY::KB + 18 * SM.body[SM.dof_cb[d]].pslot;
-    Real Sa[3], Sl[3], t[3];
     const Real *sl = lds + LY::SL + 6 * d;
-    mv3(kp, sl, Sa);
-    mv3(kp, sl + 3, Sl);
-    cross3(Sa, kp + 9, t);
+    Real K[12], sc[6];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) K[i] = kp[i];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) sc[i] = sl[i];
+    PL::rot(K); PL::col(sc);
+    Real Sa[3], Sl[3], t[3];
+    mv3m<ZR, ZW>(K, sc, Sa);
+    mv3m<ZR, ZV>(K, sc + 3, Sl);
+    cross3m<ZW, 0>(Sa, K + 9, t);
     Real *S = lds + LY::S + 6 * d;
 #pragma unroll
     for (int i = 0; i < 3; ++i) { S[i] = Sa[i]; S[3 + i] = Sl[i] - t[i]; }
@@ -738,15 +851,19 @@ DEV void kin_column(const SModel<T, Real> &SM, Real *lds, int d) {
 template <class T, typename Real>
 DEV void body_inertia(const SModel<T, Real> &SM, const DModel<Real> &M, Real *lds, int c) {
     using LY = Lay<T, Real>;
+    using PL = Planar<T>;
+    constexpr unsigned ZR = PL::ZR, ZW = PL::ZW, ZV = PL::ZV;
     const SBody<Real> &b = SM.body[c];
     const Real *kb = lds + LY::KB + 18 * c, *ab = lds + LY::AL + 6 * c;
-    Real R[9], o[3], w[3], vO[3], al[3], aO[3];
+    Real K[18], A[6];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) R[i] = kb[i];
+    for (int i = 0; i < 18; ++i) K[i] = kb[i];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) { o[i] = kb[9 + i]; w[i] = kb[12 + i]; vO[i] = kb[15 + i]; al[i] = ab[i]; aO[i] = ab[3 + i]; }
+    for (int i = 0; i < 6; ++i) A[i] = ab[i];
+    PL::frame(K); PL::acc(A);
+    const Real *R = K, *o = K + 9, *w = K + 12, *vO = K + 15, *al = A, *aO = A + 3;
     Real cl[3], cG[3];
-    mv3(R, b.com, cl);
+    mv3m<ZR, 0>(R, b.com, cl);
 #pragma unroll
     for (int i = 0; i < 3; ++i) cG[i] = o[i] + cl[i];
     Real Ib[9] = {b.inertia[0], b.inertia[3], b.inertia[4], b.inertia[3], b.inertia[1],
@@ -756,8 +873,8 @@ DEV void body_inertia(const SModel<T, Real> &SM, const DModel<Real> &M, Real *ld
     for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) RT[3 * i + j] = R[3 * j + i];
-    mm3(R, Ib, Tm);
-    mm3(Tm, RT, IG);
+    mm3m<ZR, 0>(R, Ib, Tm);
+    mm3m<0, ZR>(Tm, RT, IG);
     Real m = b.mass, ccd = dot3(cG, cG);
     Real *ic = lds + LY::IC + 10 * c;
     ic[0] = m;
@@ -770,19 +887,19 @@ DEV void body_inertia(const SModel<T, Real> &SM, const DModel<Real> &M, Real *ld
     ic[8] = IG[2] - m * cG[0] * cG[2];
     ic[9] = IG[5] - m * cG[1] * cG[2];
     Real vc[3], ac[3], t[3], t2[3];
-    cross3(w, cG, t);
+    cross3m<ZW, 0>(w, cG, t);
 #pragma unroll
     for (int i = 0; i < 3; ++i) vc[i] = vO[i] + t[i];
-    cross3(al, cG, t);
-    cross3(w, vc, t2);
+    cross3m<ZW, 0>(al, cG, t);
+    cross3m<ZW, ZV>(w, vc, t2);
 #pragma unroll
     for (int i = 0; i < 3; ++i) ac[i] = aO[i] + t[i] + t2[i];
     Real f[3], Iw[3], Ia[3], n[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) f[i] = m * (ac[i] - M.gravity[i]);
-    mv3(IG, w, Iw);
-    mv3(IG, al, Ia);
-    cross3(w, Iw, t);
+    mv3m<0, ZW>(IG, w, Iw);
+    mv3m<0, ZW>(IG, al, Ia);
+    cross3m<ZW, 0>(w, Iw, t);
 #pragma unroll
     for (int i = 0; i < 3; ++i) n[i] = Ia[i] + t[i];
     cross3(cG, f, t);
@@ -1549,7 +1666,7 @@ template <class T, typename Real> struct IdArgs {
 };
 
 template <class T, typename Real>
-__global__ __launch_bounds__(BIOIM_WG) void id_kernel(IdArgs<T, Real> a) {
+__global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))) void id_kernel(IdArgs<T, Real> a) {
     using LY = Lay<T, Real>;
     constexpr int G = T::G, ND = LY::ND, NB = T::NB, NP = LY::NP, EPB = BIOIM_WG / G;
     constexpr size_t SMB = smodel_bytes<T, Real>();
@@ -2672,7 +2789,25 @@ template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, 
 }
 
 /* structural match of a pack against a compiled topology */
+/* the pack keeps every motion in the x-y plane (tools/build_packs.py:
+ * is_planar; the PLANAR kernels carry planar frames' zeros as constants) */
+static bool pack_is_planar(const bioim_modelpack_t &p) {
+    auto zrot = [](const double *R) { return R[2] == 0 && R[5] == 0 && R[6] == 0 && R[7] == 0 && R[8] == 1; };
+    for (int c = 0; c < p.ncbody; ++c) {
+        const bioim_cbody_t &b = p.cbody[c];
+        if (!zrot(b.R_pf) || !zrot(b.R_mb)) return false;
+        for (int a = 0; a < 6; ++a) {
+            const int fi = b.fn[a];
+            if (fi < 0) continue;
+            if (a < 3 && !(b.axis[a][0] == 0 && b.axis[a][1] == 0)) return false;
+            if (a >= 3 && p.fn[fi].type != BIOIM_FN_CONST && b.axis[a][2] != 0) return false;
+        }
+    }
+    return p.gravity[2] == 0;
+}
+
 template <class T> bool topology_matches(const bioim_modelpack_t &p) {
+    if (T::PLANAR && !pack_is_planar(p)) return false;
     if (p.ncbody != T::NB || p.ndof != T::ND || p.ncoord != T::NC || p.nmuscle != T::NM || p.nact != T::NA ||
         p.nsphere != T::NS || p.ncforce != T::NF || p.nlimit != T::NL || p.nosbody != T::NOS ||
         p.n_obs_bpos != T::NOBP || p.n_obs_bvel != T::NOBV)

@@ -104,6 +104,31 @@ def unique_curves(pk):
     return seen
 
 
+def is_planar(pk):
+    """Every motion stays in the x-y plane: joint and body frames rotate
+    about z only, rotation axes that move are about z, translation axes that
+    move have no z component, gravity has none.  The kernels then carry the
+    structural zeros of planar frames (R13 R23 R31 R32 = 0, R33 = 1; angular
+    velocity/acceleration along z only; linear ones in the plane) as
+    constants (bioim_step.hip: Planar)."""
+    def zrot(R):
+        return R[2] == 0 and R[5] == 0 and R[6] == 0 and R[7] == 0 and R[8] == 1
+    for c in range(pk.ncbody):
+        b = pk.cbody[c]
+        if not (zrot(list(b.R_pf)) and zrot(list(b.R_mb))):
+            return False
+        for a in range(6):
+            fi = b.fn[a]
+            if fi < 0:
+                continue
+            ax = list(b.axis[a])
+            if a < 3 and not (ax[0] == 0 and ax[1] == 0):
+                return False
+            if a >= 3 and pk.fn[fi].type != 0 and ax[2] != 0:
+                return False
+    return pk.gravity[2] == 0
+
+
 def emit_topology(struct, pk, lanes):  # noqa: C901
     nb, nd, nc, nm = pk.ncbody, pk.ndof, pk.ncoord, pk.nmuscle
     parent = [pk.cbody[c].parent for c in range(nb)]
@@ -186,6 +211,7 @@ def emit_topology(struct, pk, lanes):  # noqa: C901
     s += f'    static constexpr int TX = {pk.coord_tx}, TY = {pk.coord_ty}, TZ = {pk.coord_tz};\n'
     s += f'    static constexpr int TORSO = {pk.torso_body}, CALCN_R = {pk.calcn_r_body}, CALCN_L = {pk.calcn_l_body};\n'
     s += f'    static constexpr unsigned FLAGS = {pk.env_flags & STRUCT_FLAGS}u; /* structural env flags */\n'
+    s += f'    static constexpr bool PLANAR = {"true" if is_planar(pk) else "false"}; /* motion in the x-y plane (is_planar) */\n'
     s += _carr('parent', parent) + _carr('anc', anc, 'unsigned') + _carr('dofmask', dofmask, 'unsigned')
     s += _carr('coord_dof', [pk.coord[c].dof for c in range(nc)])
     s += _carr('dof_cb', dof_cb) + _carr('dof_coord', dof_coord)
