@@ -908,6 +908,12 @@ DEV void body_inertia(const SModel<T, Real> &SM, const DModel<Real> &M, Real *ld
     for (int i = 0; i < 3; ++i) { wb[i] = n[i] + t[i]; wb[3 + i] = f[i]; }
 }
 
+/* symmetric 3x3 (xx yy zz xy xz yz) times v, v's known zeros masked (ZB) */
+template <unsigned ZB, typename Real> DEV void symvm(const Real *J, const Real *v, Real *o) {
+    const int r0[3] = {0, 3, 4}, r1[3] = {3, 1, 5}, r2[3] = {4, 5, 2}, iv[3] = {0, 1, 2}, sg[3] = {1, 1, 1};
+    Real x = sum_m<0, ZB, 3>(J, v, r0, iv, sg), y = sum_m<0, ZB, 3>(J, v, r1, iv, sg), z = sum_m<0, ZB, 3>(J, v, r2, iv, sg);
+    o[0] = x; o[1] = y; o[2] = z;
+}
 /* symmetric 3x3 (xx yy zz xy xz yz) times v */
 template <typename Real> DEV void symv(const Real *J, const Real *v, Real *o) {
     Real x = J[0] * v[0] + J[3] * v[1] + J[4] * v[2];
@@ -1023,12 +1029,17 @@ template <typename Real> DEV Real smooth_step_d(Real y0, Real y1, Real x0, Real 
 template <class T, typename Real>
 DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, int s, Real h) {
     using LY = Lay<T, Real>;
+    using PL = Planar<T>;
     const int cb = SM.sph_cb[s], fo = SM.sph_force[s];
-    const Real *kb = lds + LY::KB + 18 * cb;
+    const Real *kbp = lds + LY::KB + 18 * cb;
+    Real kb[18];
+#pragma unroll
+    for (int i = 0; i < 18; ++i) kb[i] = kbp[i];
+    PL::frame(kb);
     Real *cw = lds + LY::CW + 8 * s;
     Real *cj = lds + LY::CJ + LY::CJN * s;
     Real Cn[3];
-    mv3(kb, SM.sph_loc[s], Cn);
+    mv3m<PL::ZR, 0>(kb, SM.sph_loc[s], Cn);
 #pragma unroll
     for (int i = 0; i < 3; ++i) Cn[i] += kb[9 + i];
     Real rad = SM.sph_r[s];
@@ -1037,9 +1048,10 @@ DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, int s, Real h) {
     if (depth > 0) {
         P[0] = Cn[0]; P[1] = Cn[1] - (rad - Real(0.5) * depth); P[2] = Cn[2];
         Real t[3];
-        cross3(kb + 12, P, t);
+        cross3m<PL::ZW, 0>(kb + 12, P, t);
 #pragma unroll
         for (int i = 0; i < 3; ++i) vs[i] = kb[15 + i] + t[i];
+        PL::lin(vs);
         vn = -vs[1];
         Real kk = SM.cf_kk[fo];
         const Real rkd = rad * kk * depth;
@@ -1209,6 +1221,8 @@ template <class T, typename Real>
 DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const Real *lds, Real &L,
                      Real (&dLs)[T::MAXSPAN]) {
     using LY = Lay<T, Real>;
+    using PL = Planar<T>;
+    constexpr unsigned ZR = PL::ZR, ZW = PL::ZW, ZV = PL::ZV;
     constexpr int NSP = T::MAXSPAN;
     const Real *ldsq = lds + LY::QF;
     L = 0;
@@ -1221,6 +1235,7 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
         const int dk = k < mu.nspan ? mu.span[k] : 0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) Ss[k][i] = lds[LY::S + 6 * dk + i];
+        PL::col(Ss[k]);
     }
     Real Pp[3] = {0, 0, 0}, ep[3] = {0, 0, 0}, dPp[3] = {0, 0, 0};
     uint32_t maskp = 0;
@@ -1234,8 +1249,8 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
         for (int k = 0; k < NSP; ++k) {
             const int d = sd[k];
             const Real on = d >= 0 && ((maskp >> d) & 1u) ? Real(1) : Real(0);
-            const Real sm = Ss[k][0] * mo[0] + Ss[k][1] * mo[1] + Ss[k][2] * mo[2];
-            const Real sg = Ss[k][3] * g[0] + Ss[k][4] * g[1] + Ss[k][5] * g[2];
+            const Real sm = dot3m<ZW, 0>(Ss[k], mo);
+            const Real sg = dot3m<ZV, 0>(Ss[k] + 3, g);
             dLs[k] += on * (sm + sg) + (mdofp == d && d >= 0 ? gd : Real(0));
         }
     };
@@ -1268,12 +1283,16 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
                         mv3(pt.R, dl, dloc);
                     }
                 }
-                const Real *Rb = lds + LY::KB + 18 * pt.cbody;
+                const Real *kbp = lds + LY::KB + 18 * pt.cbody;
+                Real Rb[12];
+#pragma unroll
+                for (int i = 0; i < 12; ++i) Rb[i] = kbp[i];
+                PL::rot(Rb);
                 Real P[3], dP[3];
-                mv3(Rb, loc, P);
+                mv3m<ZR, 0>(Rb, loc, P);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) P[i] += Rb[9 + i];
-                mv3(Rb, dloc, dP);
+                mv3m<ZR, 0>(Rb, dloc, dP);
                 Real e[3] = {0, 0, 0};
                 if (have) {
                     Real sgm[3] = {P[0] - Pp[0], P[1] - Pp[1], P[2] - Pp[2]};
@@ -1493,20 +1512,26 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
      * inputs (S, IC, CJ, LIM) were published before the last sync, so the
      * row needs no exchange between lanes. */
     const bool implicit = h > 0;
+    using PL = Planar<T>;
+    constexpr unsigned ZW = PL::ZW, ZV = PL::ZV;
     if (lane < ND) {
-        const Real *Sd = lds + LY::S + 6 * lane, *wb = lds + LY::WB + 6 * SM.dof_cb[lane];
-        Real r = -(dot3(Sd, wb) + dot3(Sd + 3, wb + 3));
+        Real Sd[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) Sd[i] = lds[LY::S + 6 * lane + i];
+        PL::col(Sd);
+        const Real *wb = lds + LY::WB + 6 * SM.dof_cb[lane];
+        Real r = -(dot3m<ZW, 0>(Sd, wb) + dot3m<ZV, 0>(Sd + 3, wb + 3));
 #pragma unroll
         for (int i = 0; i < T::MAXARM; ++i) r += lds[LY::TAU + SM.tau_src[lane][i]];
         Real Gk[6];
         {
             const Real *ic = lds + LY::IC + 10 * SM.dof_cb[lane];
             Real t[3];
-            symv(ic + 4, Sd, Gk);
-            cross3(ic + 1, Sd + 3, t);
+            symvm<ZW>(ic + 4, Sd, Gk);
+            cross3m<0, ZV>(ic + 1, Sd + 3, t);
 #pragma unroll
             for (int i = 0; i < 3; ++i) Gk[i] += t[i];
-            cross3(Sd, ic + 1, t);
+            cross3m<ZW, 0>(Sd, ic + 1, t);
 #pragma unroll
             for (int i = 0; i < 3; ++i) Gk[3 + i] = ic[0] * Sd[3 + i] + t[i];
         }
@@ -1515,11 +1540,15 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
             constexpr unsigned msk = T::dofmask[T::sphere_cb[sp]];
             const Real *cj = lds + LY::CJ + LY::CJN * sp, *C = cj + 6;
             Real jd[3];
-            contact_jac(Sd, cj, jd);
+            cross3m<ZW, 0>(Sd, cj, jd);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) jd[i] += Sd[3 + i];
+            PL::lin(jd);
             const bool on = lds[LY::CW + 8 * sp + 6] > 0 && ((msk >> lane) & 1u);
-            r += on ? dot3(jd, cj + 3) : Real(0);
+            r += on ? dot3m<ZV, 0>(jd, cj + 3) : Real(0);
             if (implicit) {
-                Real w[3] = {C[0] * jd[0] + C[1] * jd[2], C[2] * jd[1], C[1] * jd[0] + C[3] * jd[2]};
+                Real w[3] = {(ZV & 4u) ? C[0] * jd[0] : C[0] * jd[0] + C[1] * jd[2], C[2] * jd[1],
+                             C[1] * jd[0] + C[3] * jd[2]};
                 Real pw[3];
                 cross3(cj, w, pw);
 #pragma unroll
@@ -1545,8 +1574,11 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
         sfor<0, ND>([&](auto lI) {
             constexpr int l = decltype(lI)::value;
             if ((path >> l) & 1u) {
-                const Real *Sl = lds + LY::S + 6 * l;
-                Real v = dot3(Sl, Gk) + dot3(Sl + 3, Gk + 3);
+                Real Sl[6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) Sl[i] = lds[LY::S + 6 * l + i];
+                PL::col(Sl);
+                Real v = dot3m<ZW, 0>(Sl, Gk) + dot3m<ZV, 0>(Sl + 3, Gk + 3);
                 if (implicit && l == lane) v += dg;
                 row[l] = v;
             }
