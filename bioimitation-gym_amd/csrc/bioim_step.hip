@@ -1412,25 +1412,32 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     STAMP(2);
 
     /* ---- phase 2: lane-parallel force elements */
-    {   /* subtree sums of inertia and wrench, in place (all reads, then all writes) */
+    {   /* subtree sums of inertia and wrench, in place (all reads, then all
+         * writes).  Planar models: only the components phase 3 reads against
+         * planar columns (m, h_x, h_y, J_zz; n_z, f_x, f_y) */
+        constexpr unsigned ICU = T::PLANAR ? 0x47u : 0x3FFu, WBU = T::PLANAR ? 0x1Cu : 0x3Fu;
         Real ic[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, wb[6] = {0, 0, 0, 0, 0, 0};
         if (lane < NB) {
             sfor<0, NB>([&](auto dI) {
                 constexpr int d = decltype(dI)::value;
                 if ((T::anc[d] >> lane) & 1u) {
 #pragma unroll
-                    for (int i = 0; i < 10; ++i) ic[i] += lds[LY::IC + 10 * d + i];
+                    for (int i = 0; i < 10; ++i)
+                        if ((ICU >> i) & 1u) ic[i] += lds[LY::IC + 10 * d + i];
 #pragma unroll
-                    for (int i = 0; i < 6; ++i) wb[i] += lds[LY::WB + 6 * d + i];
+                    for (int i = 0; i < 6; ++i)
+                        if ((WBU >> i) & 1u) wb[i] += lds[LY::WB + 6 * d + i];
                 }
             });
         }
         wave_sync();
         if (lane < NB) {
 #pragma unroll
-            for (int i = 0; i < 10; ++i) lds[LY::IC + 10 * lane + i] = ic[i];
+            for (int i = 0; i < 10; ++i)
+                if ((ICU >> i) & 1u) lds[LY::IC + 10 * lane + i] = ic[i];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) lds[LY::WB + 6 * lane + i] = wb[i];
+            for (int i = 0; i < 6; ++i)
+                if ((WBU >> i) & 1u) lds[LY::WB + 6 * lane + i] = wb[i];
         }
     }
     STAMP(3);
