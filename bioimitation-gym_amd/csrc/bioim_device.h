@@ -90,9 +90,11 @@ struct SBody {
     Real R_pf[9], p_pf[3], R_mb[9], p_mb[3];
     Real axis[6][3];
     Real mass, com[3], inertia[6];
-    int32_t fn[6];          /* function per spatial-transform axis (-1 none)      */
-    int32_t js[6];          /* its function slot if a spline (-1 otherwise)       */
-    int32_t parent, pslot;  /* tree parent (-1 ground); its frame slot (ground NB) */
+    Real fa[6], fb[6];      /* linear / constant axis function: a q + b, b (the
+                             * kind, coordinate and spline slot per axis are
+                             * compile-time: T::axis_kind / axis_coord,
+                             * TopoInfo::jslot) */
+    int32_t pslot, pad;     /* the parent's frame slot (ground: NB)            */
 };
 
 template <typename Real>
@@ -127,6 +129,14 @@ template <class T> struct TopoInfo {
     }
     /* function slots per dynamics call: moving-point functions, then joint splines */
     static constexpr int nslot() { return T::NMF + njs(); }
+    /* function slot of body c's spline axis a (build_smodel assigns them in
+     * body-major order after the moving-point slots), -1 if not a spline */
+    static constexpr int jslot(int c, int a) {
+        if (T::axis_kind[c * 6 + a] != BIOIM_FN_SPLINE) return -1;
+        int n = T::NMF;
+        for (int k = 0; k < c * 6 + a; ++k) n += T::axis_kind[k] == BIOIM_FN_SPLINE ? 1 : 0;
+        return n;
+    }
     static constexpr int depth_of(int c) {
         int l = 1;
         for (int p = T::parent[c]; p >= 0; p = T::parent[p]) ++l;
@@ -166,9 +176,6 @@ struct SModel {
     Real ca_opt[D::NAD], ca_min[D::NAD], ca_max[D::NAD], kp[D::NAD], kv[D::NAD];
     /* index tables */
     int32_t coord_dof[D::NCD], dof_cb[D::NDD], dof_coord[D::NDD];
-    /* packed-lower M entry e -> bytes (row l, col k, deeper dof dp (0xff:
-     * different branches, M_lk = 0), the other dof) */
-    uint32_t e_pk[D::NP];
     uint32_t dofmask[T::NB];
     /* moving-point location functions: evaluated lane-parallel once per
      * dynamics call into the env's MF slots (function index, coordinate) */

@@ -593,23 +593,41 @@ DEV void kin_local(const SModel<T, Real> &SM, Real *lds, int c) {
         constexpr int ax = decltype(aI)::value;
         cd[ax] = -1;
         if constexpr (((USED >> ax) & 1u) != 0) {
-            constexpr unsigned KM = TopoInfo<T>::axis_kinds(ax);
-            const int fi = b.fn[ax];
-            const int fs = fi >= 0 ? fi : 0;
-            const int cc = fi >= 0 ? SM.fn[fs].coord : -1;
+            /* the axis function's kind, coordinate, dof and spline slot are
+             * compile-time facts of (body, axis) (topology_matches checks kind
+             * and coordinate per pack): selected by the lane instead of read
+             * through the function table, so the coordinate and coefficient
+             * loads do not wait on one another */
+            int kind = -1, cc = -1, dof = -1, js = -1;
+            sfor<0, T::NB>([&](auto bI) {
+                constexpr int bb = decltype(bI)::value;
+                constexpr int k = T::axis_kind[bb * 6 + ax], co = T::axis_coord[bb * 6 + ax];
+                constexpr int dc = co >= 0 ? T::coord_dof[co] : -1, jsl = TopoInfo<T>::jslot(bb, ax);
+                kind = c == bb ? k : kind;
+                cc = c == bb ? co : cc;
+                dof = c == bb ? dc : dof;
+                js = c == bb ? jsl : js;
+            });
             const int cs = cc >= 0 ? cc : 0;
             Real qc = lds[LY::QF + cs], uc = lds[LY::UF + cs];
             qc = cc >= 0 ? qc : Real(0);
             uc = cc >= 0 ? uc : Real(0);
-            Real f, f1, f2;
-            fn_eval_km<KM & ~(1u << (BIOIM_FN_SPLINE + 1)), T, Real>(SM, fi, qc, f, f1, f2);
+            constexpr unsigned KM = TopoInfo<T>::axis_kinds(ax);
+            const Real fa = b.fa[ax], fb = b.fb[ax];
+            Real f = 0, f1 = 0, f2 = 0;
+            if constexpr ((KM & (1u << (BIOIM_FN_LINEAR + 1))) != 0) {
+                if (kind == BIOIM_FN_LINEAR) { f = fa * qc + fb; f1 = fa; }
+            }
+            if constexpr ((KM & (1u << (BIOIM_FN_CONST + 1))) != 0) {
+                if (kind == BIOIM_FN_CONST) f = fb;
+            }
             if constexpr ((KM & (1u << (BIOIM_FN_SPLINE + 1))) != 0) {
-                const int js = b.js[ax];   /* spline axes: evaluated in phase 0b */
-                if (js >= 0) {
-                    f = lds[LY::MF + 3 * js]; f1 = lds[LY::MF + 3 * js + 1]; f2 = lds[LY::MF + 3 * js + 2];
+                if (kind == BIOIM_FN_SPLINE) {   /* spline axes: evaluated in phase 0b */
+                    const int jj = js >= 0 ? js : 0;
+                    f = lds[LY::MF + 3 * jj]; f1 = lds[LY::MF + 3 * jj + 1]; f2 = lds[LY::MF + 3 * jj + 2];
                 }
             }
-            cd[ax] = cc >= 0 ? SM.coord_dof[cs] : -1;
+            cd[ax] = dof;
             Real a[3] = {b.axis[ax][0], b.axis[ax][1], b.axis[ax][2]};
             if constexpr (ax < 3) {
                 PL::ang(a);
@@ -625,8 +643,14 @@ DEV void kin_local(const SModel<T, Real> &SM, Real *lds, int c) {
                 }
                 PL::ang(arel); PL::ang(wrel); PL::ang(col[ax]);
                 Real Rk[9];
-                axis_rot(a, f, Rk);  /* f == 0 (absent axis): identity */
-                PL::rot(Rk);
+                if constexpr (T::PLANAR) {   /* about (0, 0, a_z), a_z = +-1 */
+                    Real sn, cn;
+                    sincos_rt(f, sn, cn);
+                    Rk[0] = cn; Rk[1] = -sn * a[2]; Rk[3] = sn * a[2]; Rk[4] = cn;
+                    PL::rot(Rk);
+                } else {
+                    axis_rot(a, f, Rk);  /* f == 0 (absent axis): identity */
+                }
                 mm3m<ZR, ZR>(RFM, Rk, RFM);
             } else {
 #pragma unroll
@@ -1799,27 +1823,34 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
         }
     }
     wave_sync();
-    if (need_m) {
-        for (int e = lane; e < NP; e += G) {
-            const uint32_t ep = SM.e_pk[e];
-            const int l = ep & 0xff, k = (ep >> 8) & 0xff, dp = (ep >> 16) & 0xff;
-            const int c = dp != 0xff ? SM.dof_cb[dp] : -1;
-            const Real *Sl = lds + LY::S + 6 * l, *Sk = lds + LY::S + 6 * k;
-            Real val = 0;
-            if (c >= 0) {
-                const Real *ic = lds + LY::IC + 10 * c;
-                Real Lm[3], Pm[3], t[3];
-                symv(ic + 4, Sl, Lm);
-                cross3(ic + 1, Sl + 3, t);
+    if (need_m && lane < ND) {
+        /* row k = lane of the packed lower M, every entry (the structural
+         * zeros too: the products below read whole rows): M_kl = S_l . I^c S_k
+         * for l on k's root path (as phase 3 of dynamics, without the
+         * implicit terms) */
+        const Real *Sd = lds + LY::S + 6 * lane, *ic = lds + LY::IC + 10 * SM.dof_cb[lane];
+        Real Gk[6], t[3];
+        symv(ic + 4, Sd, Gk);
+        cross3(ic + 1, Sd + 3, t);
 #pragma unroll
-                for (int i = 0; i < 3; ++i) Lm[i] += t[i];
-                cross3(Sl, ic + 1, t);
+        for (int i = 0; i < 3; ++i) Gk[i] += t[i];
+        cross3(Sd, ic + 1, t);
 #pragma unroll
-                for (int i = 0; i < 3; ++i) Pm[i] = ic[0] * Sl[3 + i] + t[i];
-                val = dot3(Sk, Lm) + dot3(Sk + 3, Pm);
+        for (int i = 0; i < 3; ++i) Gk[3 + i] = ic[0] * Sd[3 + i] + t[i];
+        unsigned path = 0;
+        sfor<0, ND>([&](auto kI) {
+            constexpr int k = decltype(kI)::value;
+            constexpr unsigned pm = DofTree<T>::path_mask(k);
+            path = lane == k ? pm : path;
+        });
+        Real *row = lds + LY::MP + (lane * (lane + 1)) / 2;
+        sfor<0, ND>([&](auto lI) {
+            constexpr int l = decltype(lI)::value;
+            if (l <= lane) {
+                const Real *Sl = lds + LY::S + 6 * l;
+                row[l] = ((path >> l) & 1u) ? dot3(Sl, Gk) + dot3(Sl + 3, Gk + 3) : Real(0);
             }
-            lds[LY::MP + e] = val;
-        }
+        });
     }
     if (lane < ND) lds[LY::RHS + lane] = vd;
     wave_sync();
@@ -2751,24 +2782,24 @@ template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, 
         const bioim_cbody_t &b = p.cbody[c];
         SBody<Real> &d = m.body[c];
         for (int a = 0; a < 6; ++a) {
-            d.js[a] = -1;
             const int fi = p.cbody[c].fn[a];
             if (fi >= 0 && p.fn[fi].type == BIOIM_FN_SPLINE && jslot < TopoInfo<T>::nslot()) {
-                m.mf_fn[jslot] = fi;
+                m.mf_fn[jslot] = fi;   /* slot TopoInfo<T>::jslot(c, a) */
                 m.mf_coord[jslot] = p.fn[fi].coord;
-                d.js[a] = jslot++;
+                ++jslot;
             }
         }
         for (int i = 0; i < 9; ++i) { d.R_pf[i] = (Real)b.R_pf[i]; d.R_mb[i] = (Real)b.R_mb[i]; }
         for (int i = 0; i < 3; ++i) { d.p_pf[i] = (Real)b.p_pf[i]; d.p_mb[i] = (Real)b.p_mb[i]; d.com[i] = (Real)b.com[i]; }
         for (int a = 0; a < 6; ++a) {
-            d.fn[a] = b.fn[a];
             for (int i = 0; i < 3; ++i) d.axis[a][i] = (Real)b.axis[a][i];
+            d.fa[a] = b.fn[a] >= 0 ? (Real)p.fn[b.fn[a]].a : Real(0);
+            d.fb[a] = b.fn[a] >= 0 ? (Real)p.fn[b.fn[a]].b : Real(0);
         }
         d.mass = (Real)b.mass;
         for (int i = 0; i < 6; ++i) d.inertia[i] = (Real)b.inertia[i];
-        d.parent = b.parent;
         d.pslot = b.parent >= 0 ? b.parent : T::NB;
+        d.pad = 0;
         constexpr int DEP = TopoInfo<T>::depth();
         int path[DEP], n = 0;
         for (int q = c; q >= 0 && n < DEP; q = p.cbody[q].parent) path[n++] = q;
@@ -2818,13 +2849,6 @@ template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, 
         m.os_cb[b] = p.osbody[b].cbody;
         for (int i = 0; i < 3; ++i) m.os_p[b][i] = (Real)p.osbody[b].p[i];
     }
-    for (int l = 0, e = 0; l < p.ndof; ++l)
-        for (int k = 0; k <= l; ++k, ++e) {
-            int cl = m.dof_cb[l], ck = m.dof_cb[k];
-            const int c = ((T::anc[cl] >> ck) & 1u) ? cl : (((T::anc[ck] >> cl) & 1u) ? ck : -1);
-            const int dp = c < 0 ? 0xff : (c == cl ? l : k), ot = c < 0 ? 0 : (c == cl ? k : l);
-            m.e_pk[e] = (uint32_t)l | ((uint32_t)k << 8) | ((uint32_t)dp << 16) | ((uint32_t)ot << 24);
-        }
 }
 
 /* structural match of a pack against a compiled topology */
