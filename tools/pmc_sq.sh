@@ -7,7 +7,7 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_${TAG}_fp${PREC}
 [ -z "$GRAFT_REPO_ROOT" ] && OUT=$(pwd)/gpurun_out/pmc_${TAG}_fp${PREC}
 mkdir -p $OUT
 export BIOIM_PRECISION=$PREC
-ARGS="--steps 5 --warmup 2 --no-cpu-baseline"
+ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-reference-integrator"
 i=0
 for G in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
          "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM" \

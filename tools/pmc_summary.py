@@ -8,7 +8,7 @@ import sys
 d = sys.argv[1]
 vals = {}
 for f in sorted(glob.glob(os.path.join(d, 'p*', '*counter_collection.csv'))):
-    rows = [r for r in csv.DictReader(open(f)) if 'env_kernel' in r['Kernel_Name']]
+    rows = [r for r in csv.DictReader(open(f)) if 'env_kernel' in r['Kernel_Name'] and 'false, false>' in r['Kernel_Name']]   # the default (no push, semi-implicit) kernel
     disp = sorted({int(r['Dispatch_Id']) for r in rows})[1:]
     for r in rows:
         if int(r['Dispatch_Id']) in disp:
