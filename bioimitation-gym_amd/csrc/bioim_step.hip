@@ -599,14 +599,22 @@ DEV void kin_local(const SModel<T, Real> &SM, Real *lds, int c) {
              * through the function table, so the coordinate and coefficient
              * loads do not wait on one another */
             int kind = -1, cc = -1, dof = -1, js = -1;
+            /* spatial models: an opaque copy of the lane's body, so the
+             * selects are recomputed per call (a few VALU ops) instead of
+             * hoisted out of the substep loop into 24 registers live across
+             * it (the 3D push + RK-Merson kernel otherwise spills 16 B; 1 %
+             * slower in 3D, so the planar kernels, far from the register
+             * limit, keep the hoisted copies) */
+            int cb = c;
+            if constexpr (!T::PLANAR) asm volatile("" : "+v"(cb));
             sfor<0, T::NB>([&](auto bI) {
                 constexpr int bb = decltype(bI)::value;
                 constexpr int k = T::axis_kind[bb * 6 + ax], co = T::axis_coord[bb * 6 + ax];
                 constexpr int dc = co >= 0 ? T::coord_dof[co] : -1, jsl = TopoInfo<T>::jslot(bb, ax);
-                kind = c == bb ? k : kind;
-                cc = c == bb ? co : cc;
-                dof = c == bb ? dc : dof;
-                js = c == bb ? jsl : js;
+                kind = cb == bb ? k : kind;
+                cc = cb == bb ? co : cc;
+                dof = cb == bb ? dc : dof;
+                js = cb == bb ? jsl : js;
             });
             const int cs = cc >= 0 ? cc : 0;
             Real qc = lds[LY::QF + cs], uc = lds[LY::UF + cs];
