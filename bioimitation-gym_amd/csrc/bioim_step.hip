@@ -205,7 +205,7 @@ template <int G> DEV bool group_any(bool p) {
 }
 
 #ifdef BIOIM_STAMPS
-__device__ unsigned long long g_stamps[16];
+__device__ unsigned long long g_stamps[24];
 #endif
 
 /* ------------------------------------------------------------ functions */
@@ -1058,8 +1058,18 @@ template <typename Real> DEV Real smooth_step_d(Real y0, Real y1, Real x0, Real 
  * implicit damping/stiffness block C (h > 0) into CJ.  Phase 3 forms the
  * contact-point Jacobian J_d = S_d.ang x P + S_d.lin from the Plucker
  * columns it already holds: M_lk += J_l.C J_k, rhs_d += S_d.(P x F, F). */
+/* One sphere's Hunt-Crossley contact (lane = sphere s): the force and its
+ * moment about the ground origin (CW slot: F3, Mo3, active), and for the
+ * implicit step the contact point, the force with the -h Kn v_y term and
+ * the 3x3 damping/stiffness block (CJ slot).  Branch-free (selects only), so
+ * the muscle lanes can evaluate it inside the muscle block where the
+ * scheduler interleaves it with the curve evaluations' dependency chains
+ * (contact_store writes it); an inactive sphere's CJ values are unused. */
+template <typename Real> struct ContactOut {
+    Real cw[7], cj[10];
+};
 template <class T, typename Real>
-DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, int s, Real h) {
+DEV void contact_compute(const SModel<T, Real> &SM, const Real *lds, int s, Real h, ContactOut<Real> &o) {
     using LY = Lay<T, Real>;
     using PL = Planar<T>;
     const int cb = SM.sph_cb[s], fo = SM.sph_force[s];
@@ -1068,80 +1078,76 @@ DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, int s, Real h) {
 #pragma unroll
     for (int i = 0; i < 18; ++i) kb[i] = kbp[i];
     PL::frame(kb);
-    Real *cw = lds + LY::CW + 8 * s;
-    Real *cj = lds + LY::CJ + LY::CJN * s;
     Real Cn[3];
     mv3m<PL::ZR, 0>(kb, SM.sph_loc[s], Cn);
 #pragma unroll
     for (int i = 0; i < 3; ++i) Cn[i] += kb[9 + i];
-    Real rad = SM.sph_r[s];
-    Real depth = rad - Cn[1];
-    Real fn = 0, fH = 0, vn = 0, P[3] = {0, 0, 0}, vs[3] = {0, 0, 0};
-    if (depth > 0) {
-        P[0] = Cn[0]; P[1] = Cn[1] - (rad - Real(0.5) * depth); P[2] = Cn[2];
-        Real t[3];
-        cross3m<PL::ZW, 0>(kb + 12, P, t);
+    const Real rad = SM.sph_r[s];
+    const Real depth = rad - Cn[1];
+    const bool pen = depth > 0;
+    const Real P[3] = {Cn[0], Cn[1] - (rad - Real(0.5) * depth), Cn[2]};
+    Real t[3], vs[3];
+    cross3m<PL::ZW, 0>(kb + 12, P, t);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) vs[i] = kb[15 + i] + t[i];
-        PL::lin(vs);
-        vn = -vs[1];
-        Real kk = SM.cf_kk[fo];
-        const Real rkd = rad * kk * depth;
-        fH = Real(4.0 / 3.0) * kk * depth * (rkd * fast_rsqrt(rkd));
-        fn = fH * (Real(1) + Real(1.5) * SM.cf_c[fo] * vn);
-    }
-    bool active = fn > 0;
-    cw[6] = active ? Real(1) : Real(0);
-    if (!active) {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) cw[i] = 0;
-        return;
-    }
-    Real F[3] = {0, fn, 0};
-    Real vt0 = -vs[0], vt2 = -vs[2];
+    for (int i = 0; i < 3; ++i) vs[i] = kb[15 + i] + t[i];
+    PL::lin(vs);
+    const Real vn = -vs[1];
+    const Real kk = SM.cf_kk[fo], cc = SM.cf_c[fo];
+    const Real dps = pen ? depth : Real(1);
+    const Real rkd = rad * kk * dps;
+    const Real fH = pen ? Real(4.0 / 3.0) * kk * dps * (rkd * fast_rsqrt(rkd)) : Real(0);
+    const Real fn = fH * (Real(1) + Real(1.5) * cc * vn);
+    const bool active = pen && fn > 0;
+    const Real vt0 = -vs[0], vt2 = -vs[2];
     const Real vs2 = vt0 * vt0 + vt2 * vt2;
-    const Real ivs_ = vs2 > 0 ? fast_rsqrt(vs2) : Real(0);
-    Real vslip = vs2 * ivs_;
-    Real vtr = SM.cf_vt[fo], ms = SM.cf_ms[fo], md = SM.cf_md[fo], mv = SM.cf_mv[fo];
+    const Real ivs = vs2 > 0 ? fast_rsqrt(vs2) : Real(0);
+    const Real vslip = vs2 * ivs;
+    const Real vtr = SM.cf_vt[fo], ms = SM.cf_ms[fo], md = SM.cf_md[fo], mv = SM.cf_mv[fo];
     const Real ivtr = fast_rcp(vtr);
-    Real r_ = vslip * ivtr, den = Real(1) + r_ * r_;
-    const Real iden = fast_rcp(den), ivs = ivs_;
-    if (vslip != 0) {
-        Real ff = fn * (fmin(r_, Real(1)) * (md + Real(2) * (ms - md) * iden) + mv * vslip);
-        F[0] += ff * vt0 * ivs;
-        F[2] += ff * vt2 * ivs;
-    }
+    const Real r_ = vslip * ivtr, den = Real(1) + r_ * r_;
+    const Real iden = fast_rcp(den);
+    const Real ff = fn * (fmin(r_, Real(1)) * (md + Real(2) * (ms - md) * iden) + mv * vslip);
+    const bool slip = vslip != 0;
+    Real F[3] = {slip ? ff * vt0 * ivs : Real(0), fn, slip ? ff * vt2 * ivs : Real(0)};
     Real mo[3];
     cross3(P, F, mo);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) { cw[i] = F[i]; cw[3 + i] = mo[i]; }
-    Real kn = Real(1.5) * fH * fast_rcp(depth) * (Real(1) + Real(1.5) * SM.cf_c[fo] * vn);
+    for (int i = 0; i < 3; ++i) { o.cw[i] = active ? F[i] : Real(0); o.cw[3 + i] = active ? mo[i] : Real(0); }
+    o.cw[6] = active ? Real(1) : Real(0);
+    const Real kn = Real(1.5) * fH * fast_rcp(dps) * (Real(1) + Real(1.5) * cc * vn);
     /* implicit extra force -h*Kn*v_y (Hertz force at the advanced position) */
 #pragma unroll
-    for (int i = 0; i < 3; ++i) cj[i] = P[i];
-    cj[3] = F[0];
-    cj[4] = F[1] - (h > 0 ? h * kn * vs[1] : Real(0));
-    cj[5] = F[2];
-    Real cxx = 0, cxz = 0, cyy = 0, czz = 0;
-    if (h > 0) {
-        Real g_s, gp;
-        if (r_ < 1) {
-            g_s = (md + Real(2) * (ms - md) * iden) * ivtr + mv;
-            gp = (md + Real(2) * (ms - md) * iden) * ivtr - Real(4) * (ms - md) * r_ * r_ * (iden * iden * ivtr) + mv;
-        } else {
-            g_s = (md + Real(2) * (ms - md) * iden) * ivs + mv;
-            gp = -Real(4) * (ms - md) * r_ * (iden * iden * ivtr) + mv;
-        }
-        gp = gp < 0 ? Real(0) : gp;
-        Real tx = 0, tz = 0;
-        if (vslip > 0) { tx = vt0 * ivs; tz = vt2 * ivs; }
-        Real ctt = h * fn * g_s, cq = h * fn * (gp - g_s);
-        cyy = h * Real(1.5) * SM.cf_c[fo] * fH + h * h * kn;
-        cxx = ctt + cq * tx * tx;
-        cxz = cq * tx * tz;
-        czz = ctt + cq * tz * tz;
-    }
-    cj[6] = cxx; cj[7] = cxz; cj[8] = cyy; cj[9] = czz;
+    for (int i = 0; i < 3; ++i) o.cj[i] = P[i];
+    o.cj[3] = F[0];
+    o.cj[4] = F[1] - (h > 0 ? h * kn * vs[1] : Real(0));
+    o.cj[5] = F[2];
+    const Real base = (md + Real(2) * (ms - md) * iden);
+    const bool low = r_ < 1;
+    Real g_s = low ? base * ivtr + mv : base * ivs + mv;
+    Real gp = low ? base * ivtr - Real(4) * (ms - md) * r_ * r_ * (iden * iden * ivtr) + mv
+                  : -Real(4) * (ms - md) * r_ * (iden * iden * ivtr) + mv;
+    gp = gp < 0 ? Real(0) : gp;
+    const Real tx = vslip > 0 ? vt0 * ivs : Real(0), tz = vslip > 0 ? vt2 * ivs : Real(0);
+    const Real ctt = h * fn * g_s, cq = h * fn * (gp - g_s);
+    const bool imp = h > 0;
+    o.cj[6] = imp ? ctt + cq * tx * tx : Real(0);
+    o.cj[7] = imp ? cq * tx * tz : Real(0);
+    o.cj[8] = imp ? h * Real(1.5) * cc * fH + h * h * kn : Real(0);
+    o.cj[9] = imp ? ctt + cq * tz * tz : Real(0);
+}
+template <class T, typename Real> DEV void contact_store(Real *lds, int s, const ContactOut<Real> &o) {
+    using LY = Lay<T, Real>;
+    Real *cw = lds + LY::CW + 8 * s, *cj = lds + LY::CJ + LY::CJN * s;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) cw[i] = o.cw[i];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) cj[i] = o.cj[i];
+}
+template <class T, typename Real>
+DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, int s, Real h) {
+    ContactOut<Real> o;
+    contact_compute<T, Real>(SM, lds, s, h, o);
+    contact_store<T, Real>(lds, s, o);
 }
 
 /* contact-point Jacobian column of a dof: S.ang x P + S.lin */
@@ -1160,6 +1166,7 @@ template <typename Real> struct MState {
 template <class T, typename Real>
 DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_state, Real l_state, Real excitation,
                      Real L, Real v_warm, MState<Real> &s) {
+    STAMP_DECL
     const DCurve<Real> &Cfal = SM.curve[mu.cv[0]], &Cfv = SM.curve[mu.cv[1]], &Cfpe = SM.curve[mu.cv[2]],
                        &Cfse = SM.curve[mu.cv[3]];
     Real a = a_state < mu.amin ? mu.amin : (a_state > Real(1) ? Real(1) : a_state);
@@ -1174,8 +1181,10 @@ DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_
     curve_eval(Cfal, lce * mu.inv_lopt, fal, dfal);
     curve_eval(Cfpe, lce * mu.inv_lopt, fpe, dfpe);
     Real rhs = fse * icos - fpe;
+    STAMP(16);
     Real vN, fvv, dfv;
     solve_fv(Cfv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
+    STAMP(17);
     Real dGdv = a * fal * dfv + mu.beta;
     bool clamped = (l_state <= mu.lmin && vN <= 0) || l_state < mu.lmin;
     if (clamped) {
@@ -1196,6 +1205,7 @@ DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_
     const Real ab = Real(0.5) + Real(1.5) * a;
     /* du/dt = (u - a) / tau, tau = tau_act (0.5 + 1.5 a) or tau_deact / (0.5 + 1.5 a) */
     s.dadt = u > a ? (u - a) * fast_rcp(mu.tau_act * ab) : (u - a) * ab * fast_rcp(mu.tau_deact);
+    STAMP(18);
 }
 
 /* static fiber equilibrium at reset (zero fiber velocity) */
@@ -1473,6 +1483,10 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
         }
     }
     STAMP(3);
+    /* contacts computed by the first muscle pass when every sphere lane
+     * holds a muscle there */
+    constexpr bool MUSCLE_CONTACT = T::NM >= T::NS && T::NS > 0;
+    ContactOut<Real> CO;
     if constexpr (T::NM > 0) {
         /* this lane's muscles' -F_t dL/dq over their spans, stored per muscle
          * slot and span entry (plain stores); the dof lanes gather them in
@@ -1496,6 +1510,10 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
                 }
                 D.act[j] = a_;
                 D.lce[j] = l_;
+                /* the sphere contacts ride in the first muscle pass (every
+                 * sphere lane holds a muscle): same block as the curve
+                 * evaluations, so their chains interleave */
+                if constexpr (j == 0 && MUSCLE_CONTACT) contact_compute<T, Real>(SM, lds, lane < T::NS ? lane : 0, h, CO);
                 muscle_eval<T, Real>(SM, mu, a_, l_, control[j], L, D.ms[j].vN, D.ms[j]);
                 const Real nFt = -D.ms[j].Ft;
                 Real *ts = lds + LY::TAU + (lane + j * G) * T::MAXSPAN;
@@ -1513,7 +1531,11 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
         });
     }
     STAMP(5);
-    if (lane < T::NS) contact_lane<T, Real>(SM, lds, lane, h);
+    if constexpr (MUSCLE_CONTACT) {
+        if (lane < T::NS) contact_store<T, Real>(lds, lane, CO);
+    } else {
+        if (lane < T::NS) contact_lane<T, Real>(SM, lds, lane, h);
+    }
     STAMP(6);
     if (lane < T::NL) {
         int cc = SM.lim_coord[lane];
@@ -3530,9 +3552,9 @@ int bioim_set_stream(bioim_handle_t *h, void *s) {
 #ifdef BIOIM_STAMPS
 int bioim_debug_stamps(unsigned long long *out, int reset) {
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16));
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 24));
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[24] = {0};
         HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)));
     }
     return 0;
