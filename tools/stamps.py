@@ -14,7 +14,7 @@ f = L.bioim_debug_stamps
 f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 env = VectorEnv(env_id, 4096, precision=prec, seed=1, auto_reset=True)
 env.reset()
-buf = (C.c_ulonglong * 16)()
+buf = (C.c_ulonglong * 24)()
 steps = 30
 steps = 30
 acts = torch.rand((steps + 5, 4096, env.action_dim), device=env.device, dtype=env.dtype)
@@ -39,3 +39,6 @@ print(f'  per launch: loop {buf[10] / steps:.0f} cyc, of which dynamics {tot / s
 if buf[13]:
     print(f'  solve_fv (wg 0, env 0 lanes): mean iterations {buf[12] / buf[13]:.2f} over {buf[13]} solves, '
           f'{buf[14]} hit it_max')
+if buf[16] or buf[17]:
+    print(f'  muscle eval of lane 0 (wg 0, env 0), per dynamics call: curves + pennation {buf[16] / calls:.0f} cyc, '
+          f'fiber-velocity solve {buf[17] / calls:.0f} cyc, rest {buf[18] / calls:.0f} cyc')
