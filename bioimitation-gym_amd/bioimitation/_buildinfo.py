@@ -18,7 +18,8 @@ REPO = os.path.dirname(PKG_ROOT)
 CSRC = os.path.join(PKG_ROOT, 'csrc')
 INCLUDE = os.path.join(REPO, 'include')
 SOURCES = [os.path.join(CSRC, f) for f in ('bioim_step.hip', 'bioim_device.h', 'topologies.h')] + \
-    [os.path.join(INCLUDE, f) for f in ('bioim.h', 'bioim_modelpack.h')]
+    [os.path.join(INCLUDE, f) for f in ('bioim.h', 'bioim_modelpack.h')] + \
+    [os.path.join(REPO, '__graft_entry__.py')]   # the per-object -D unit selectors and the link line live there
 
 # LLVM's iterative ILP machine scheduler for gfx950: the step kernel runs one
 # wave per SIMD and is latency-bound, and this schedule shortens its dependent
@@ -37,8 +38,13 @@ def hipcc_flags(extra=()):
                    '-Wno-unused-result', '-Wno-unused-value'] + SCHED + list(extra)
 
 
+def sources_present():
+    return all(os.path.exists(f) for f in SOURCES)
+
+
 def build_id(extra=()):
-    """sha256 over the kernel sources and the compile flags, 16 hex digits."""
+    """sha256 over the kernel sources, the build recipe and the compile
+    flags, 16 hex digits."""
     h = hashlib.sha256()
     for f in SOURCES:
         h.update(os.path.basename(f).encode())

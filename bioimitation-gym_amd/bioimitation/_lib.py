@@ -84,6 +84,11 @@ def check_build_id(L):
     from . import _buildinfo
     if 'BIOIM_LIB' in os.environ:
         return
+    if not _buildinfo.sources_present():
+        # a library shipped without its sources (installed elsewhere): nothing to compare against
+        import warnings
+        warnings.warn(f'{LIB_PATH}: kernel sources not found next to the library; build id not checked')
+        return
     got = L.bioim_build_id().decode()
     want = _buildinfo.build_id()
     if got != want:

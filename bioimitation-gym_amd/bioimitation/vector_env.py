@@ -28,6 +28,25 @@ from .registry import load_pack
 INTEGRATORS = {'semi-implicit': 0, 'rk-merson': 1}
 
 
+def check_env_mask(mask, num_envs, device):
+    """A per-env mask the step kernel may read: a contiguous (num_envs,)
+    uint8/bool tensor on the env's device (or None).  Anything else would
+    make the kernel read host memory or past the end of the buffer."""
+    import torch
+    if mask is None:
+        return
+    if not isinstance(mask, torch.Tensor):
+        raise ValueError('env mask must be a torch tensor (or None)')
+    if mask.dtype not in (torch.uint8, torch.bool):
+        raise ValueError(f'env mask dtype must be uint8 or bool, got {mask.dtype}')
+    if mask.device != torch.device(device):
+        raise ValueError(f'env mask must be on {device}, got {mask.device}')
+    if mask.dim() != 1 or mask.numel() != num_envs:
+        raise ValueError(f'env mask must have shape ({num_envs},), got {tuple(mask.shape)}')
+    if not mask.is_contiguous():
+        raise ValueError('env mask must be contiguous')
+
+
 class VectorEnv:
     def __init__(self, env_id: str, num_envs: int, config: dict = None, device: int = 0, precision: int = 64,
                  seed: int = 0, auto_reset: bool = False, env_offset: int = 0):
@@ -151,6 +170,7 @@ class VectorEnv:
         tensor read by every later ``step()``; envs with 0 are left untouched
         unless they are finishing a suspended RK step.  ``None`` steps all.
         The tensor must stay alive while it is set."""
+        check_env_mask(mask, self.num_envs, self.device)
         self._active = mask
         _lib.check(self._L.bioim_set_active_mask(self._h, self._ptr(mask)))
 

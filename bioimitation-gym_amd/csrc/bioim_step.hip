@@ -3171,6 +3171,11 @@ template <typename Real> int xfer_state(bioim_handle_t *h, double *host, const d
     DState<Real> hs;
     state_layout<Real>(h, buf.data(), &hs);
     int dim = bioim_state_dim(h);
+    if (host)
+        for (size_t e = 0; e < n; ++e)
+            if (hs.pend[e])   /* mid-step: t is the step's end time but q/u/act/lce an accepted RK point */
+                return fail(BIOIM_E_ARG, "bioim_get_state: envs are suspended mid-step by the RK budget "
+                                         "(step until bioim_pending_count() is 0)");
     for (size_t e = 0; e < n; ++e) {
         if (host) {
             double *s = host + e * dim;
@@ -3349,6 +3354,18 @@ int bioim_set_rk_budget(bioim_handle_t *h, int attempts, uint8_t *ready_out) {
 
 int bioim_set_active_mask(bioim_handle_t *h, const uint8_t *active) {
     if (!h) return fail(BIOIM_E_ARG, "null handle");
+    if (active) {
+        /* the step kernel reads active[env] for every env: refuse host memory
+         * and memory of another device (a GPU fault otherwise); the length
+         * (n bytes) is the caller's contract, checked by VectorEnv */
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, active) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(BIOIM_E_ARG, "bioim_set_active_mask: not a device pointer");
+        }
+        if (at.type != hipMemoryTypeDevice || at.device != h->device)
+            return fail(BIOIM_E_ARG, "bioim_set_active_mask: mask must be device memory on the handle's device");
+    }
     h->active = active;
     return 0;
 }
@@ -3357,6 +3374,7 @@ int bioim_pending_count(bioim_handle_t *h) {
     if (!h) return fail(BIOIM_E_ARG, "null handle");
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipStreamSynchronize(h->side));   /* a group step may have run this handle on its side stream */
     std::vector<int32_t> p(h->n);
     const int32_t *dp = h->precision == 64 ? reinterpret_cast<DState<double> *>(h->dstate)->pend
                                            : reinterpret_cast<DState<float> *>(h->dstate)->pend;

@@ -87,3 +87,44 @@ def test_create_rejects_a_pack_with_a_bad_magic():
     h = C.c_void_p()
     assert L.bioim_create(C.byref(pk), 4, 0, 64, 0, C.byref(h)) == -3     # BIOIM_E_PACK
     assert b'magic' in L.bioim_last_error()
+
+
+def test_env_mask_validation_refuses_what_the_kernel_cannot_read():
+    """VectorEnv.set_active_mask hands the mask's pointer to the step kernel,
+    which reads one byte per env: a wrong dtype, device, length, shape or a
+    non-contiguous view is refused before it reaches the library."""
+    import torch
+    from bioimitation.vector_env import check_env_mask
+    dev = torch.device('cuda', 0)
+    check_env_mask(None, 8, dev)
+    with pytest.raises(ValueError, match='dtype'):
+        check_env_mask(torch.zeros(8, dtype=torch.int64), 8, dev)
+    with pytest.raises(ValueError, match='dtype'):
+        check_env_mask(torch.zeros(8, dtype=torch.float32), 8, dev)
+    with pytest.raises(ValueError, match='must be on'):
+        check_env_mask(torch.zeros(8, dtype=torch.uint8), 8, dev)            # a CPU tensor
+    with pytest.raises(ValueError, match='torch tensor'):
+        check_env_mask([1] * 8, 8, dev)
+    cpu = torch.device('cpu')      # the remaining checks, on a device this machine has
+    with pytest.raises(ValueError, match='shape'):
+        check_env_mask(torch.zeros(7, dtype=torch.uint8), 8, cpu)
+    with pytest.raises(ValueError, match='shape'):
+        check_env_mask(torch.zeros((2, 4), dtype=torch.bool), 8, cpu)
+    with pytest.raises(ValueError, match='contiguous'):
+        check_env_mask(torch.zeros(16, dtype=torch.uint8)[::2], 8, cpu)
+    check_env_mask(torch.zeros(8, dtype=torch.bool), 8, cpu)
+
+
+def test_set_active_mask_refuses_a_host_pointer():
+    """The raw C entry refuses host memory (hipPointerGetAttributes) instead
+    of letting the kernel read it; a null handle is an argument error."""
+    _lib, L = _lib_or_skip()
+    assert L.bioim_set_active_mask(None, None) == -1
+
+
+def test_build_id_covers_the_build_recipe():
+    """The per-object -D unit selectors and the link line live in
+    __graft_entry__.py, so it is part of the build id."""
+    from bioimitation import _buildinfo
+    assert any(p.endswith('__graft_entry__.py') for p in _buildinfo.SOURCES)
+    assert _buildinfo.sources_present()

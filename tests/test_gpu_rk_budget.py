@@ -91,8 +91,13 @@ def test_rk_budget_state_roundtrip_clears_pending():
     assert env.pending_count() > 0
     with pytest.raises(_lib.BioimError):
         _lib.check(env._L.bioim_set_integrator(env._h, 0, 0.0))
+    # a suspended env's state is not at a step boundary (t is the step's end
+    # time, q/u/act/lce an accepted point inside it): get_state refuses it
+    with pytest.raises(_lib.BioimError, match='suspended'):
+        env.get_state()
     env.set_state(s)
     assert env.pending_count() == 0
+    np.testing.assert_array_equal(env.get_state(), s)
     env.close()
 
 
