@@ -108,6 +108,8 @@ class ImitationEnv:
         from .obslayout import load_names
         from .simulation_io import OsimModelFacade
         self.osim_model = OsimModelFacade(self._env, load_names(self.env_id), lo, hi)
+        self._last = None            # (reward, all_rewards, done) of the last step
+        self.state_dict = None
         self._record = bool(cfg.get('record_trajectory', True))
         if self._record:
             self._env.enable_force_report()
@@ -132,7 +134,9 @@ class ImitationEnv:
     def reset(self, obs_as_dict=False):
         index = 0 if self.test else random.randint(0, self._env.pack.reset_hi)
         obs = self._env.reset(env_ids=[0], ref_index=[index])
+        self.osim_model._dirty()
         self.osim_model.recorder.clear()     # reset_manager re-initializes the analyses
+        self._last = None
         self._record_row(obs)
         return self._out(obs, obs_as_dict)
 
@@ -141,10 +145,68 @@ class ImitationEnv:
         a = torch.as_tensor(np.asarray(action, dtype=np.float64).reshape(1, -1), dtype=self._env.dtype,
                             device=self._env.device)
         obs, rew, done, info = self._env.step(a)
+        self.osim_model._dirty()
         self._record_row(obs)
-        info = info[0].double().cpu().numpy()
-        return [self._out(obs, obs_as_dict), float(rew[0]), bool(done[0]),
-                {'all_rewards': [float(v) for v in info]}]
+        info = [float(v) for v in info[0].double().cpu().numpy()]
+        self._last = (float(rew[0]), info, bool(done[0]))
+        return [self._out(obs, obs_as_dict), self._last[0], self._last[2], {'all_rewards': info}]
+
+    # -- the task envs' public methods (muscle_walking_imitation_env2D.py:102-403,
+    #    opensim_environment.py:52-98); realizations run on the GPU (bioim_osim) --
+    def get_state_dict(self):
+        """The observation dict at the current state (obs_as_dict layout); also
+        sets ``self.state_dict`` to the merged calc_* realizations, as the
+        reference does (:158-230)."""
+        om = self.osim_model
+        self.state_dict = {}
+        for part in (om.calc_joint_kinematics(), om.calc_body_kinematics(), om.calc_muscles_info(),
+                     om.calc_forces_info()):
+            self.state_dict.update(part)
+        return self._out(om.observation()[None, :], True)
+
+    def get_observation_dict(self):
+        return self.get_state_dict()
+
+    def get_observation(self):
+        """the flattened observation (opensim_environment.py:52-64), a list"""
+        return [float(v) for v in self.osim_model.observation()]
+
+    def get_reward(self):
+        """(reward, all_rewards) of the last step.  The reference recomputes it
+        and advances its cross-step terms (last action, old pelvis x) as a side
+        effect; here those advance inside the step kernel, so this returns the
+        step's values and changes nothing."""
+        if self._last is None:
+            raise RuntimeError('get_reward: no step since the last reset')
+        return self._last[0], list(self._last[1])
+
+    def is_done(self):
+        """the termination flag of the last step (False before any step)"""
+        return bool(self._last[2]) if self._last is not None else False
+
+    def get_limit_forces(self):
+        """muscle_walking_imitation_env2D.py:232-235"""
+        return list(self.osim_model.calc_forces_info()['coordinate_limit_forces'].values())
+
+    def calc_cost_of_transport(self):
+        """Umberger-style metabolic rate of the realized state
+        (muscle_walking_imitation_env2D.py:360-403), computed on the GPU; muscle
+        models only, like the reference."""
+        if not self.osim_model.is_muscle_model:
+            raise AttributeError(f'{type(self).__name__} has no calc_cost_of_transport (torque model)')
+        return self.osim_model.report()['cot']
+
+    def get_mass(self):
+        self.mass = self.osim_model.model.getTotalMass(self.osim_model.state)
+        return self.mass
+
+    def get_height(self):
+        self.height = 1.80   # hard-coded in every reference env (:106-109)
+        return self.height
+
+    def get_gravity(self):
+        self.gravity = self.osim_model.model.getGravity()
+        return self.gravity
 
     def render(self, mode='human', close=False):
         return

@@ -129,30 +129,319 @@ class TrajectoryRecorder:
         return [coords[self.pack.coordact[a].coord] for a in range(self.pack.nact)]
 
 
-class OsimModelFacade:
-    """The slice of ``OsimModel`` (opensim_wrapper.py:6-338) that callers of
-    the reference touch from outside the env: ``istep``, ``step_size``,
-    ``action_min/max``, ``coordinate_names``, ``muscle_names``,
-    ``is_muscle_model``, ``get_action_space_size()`` and
-    ``save_simulation(base_dir)`` (tests/sample_rllib_testing.py:71,
-    tests/example_position_control.py:312).  It is backed by one env of a
-    :class:`~bioimitation.vector_env.VectorEnv`."""
+def split_osim_report(pk, row) -> dict:
+    """One env's ``bioim_osim`` report row (include/bioim.h layout) as named
+    arrays: time, istep, q/u/qdd (CoordinateSet order), bodies (NOS, 18: pos,
+    vel, acc, body-fixed XYZ angles, angular vel, angular acc), com (9: pos,
+    vel, acc), muscles (NM, 7: activation, fiber length, fiber velocity, fiber
+    force, active fiber force, excitation, tendon force), actuation (NA),
+    contact (NF, 6: force, moment on the feet), limits (NL), cot."""
+    row = np.asarray(row, dtype=np.float64)
+    nc, nb, nm, na, nf, nl = pk.ncoord, pk.nosbody, pk.nmuscle, pk.nact, pk.ncforce, pk.nlimit
+    r, k = {'time': float(row[0]), 'istep': int(round(row[1]))}, 2
+    for key, n in (('q', nc), ('u', nc), ('qdd', nc)):
+        r[key], k = row[k:k + n], k + n
+    r['bodies'], k = row[k:k + 18 * nb].reshape(nb, 18), k + 18 * nb
+    r['com'], k = row[k:k + 9], k + 9
+    r['muscles'], k = row[k:k + 7 * nm].reshape(nm, 7), k + 7 * nm
+    r['actuation'], k = row[k:k + na], k + na
+    r['contact'], k = row[k:k + 6 * nf].reshape(nf, 6), k + 6 * nf
+    r['limits'], k = row[k:k + nl], k + nl
+    r['cot'] = float(row[k])
+    assert k + 1 == len(row), (k + 1, len(row))
+    return r
 
-    def __init__(self, env, names, action_min, action_max):
+
+class _Muscle:
+    def __init__(self, name, mu):
+        self._name, self._mu = name, mu
+
+    def getName(self):
+        return self._name
+
+    def getMaxIsometricForce(self):
+        return float(self._mu.fiso)
+
+    def getOptimalFiberLength(self):
+        return float(self._mu.lopt)
+
+
+class _Set(list):
+    def getSize(self):
+        return len(self)
+
+    def get(self, i):
+        return self[i]
+
+
+class ModelView:
+    """The slice of ``opensim.Model`` the task envs read through
+    ``osim_model.model`` (getTotalMass, getGravity, getMuscles:
+    muscle_walking_imitation_env2D.py:102-113, 360-403), from the ModelPack."""
+
+    def __init__(self, pack, names):
+        self._pack, self._names = pack, names
+
+    def getTotalMass(self, state=None):
+        return float(self._pack.total_mass)
+
+    def getGravity(self):
+        return [float(self._pack.gravity[i]) for i in range(3)]
+
+    def getMuscles(self):
+        pk = self._pack
+        return _Set(_Muscle(n, pk.muscle[i]) for i, n in enumerate(self._names['muscles'][:pk.nmuscle]))
+
+
+class OsimModelFacade:
+    """``OsimModel`` (opensim_wrapper.py:6-338) over one env of a
+    :class:`~bioimitation.vector_env.VectorEnv`: the fields
+    (``istep``, ``step_size``, ``action_min/max``, ``coordinate_names``,
+    ``muscle_names``, ``is_muscle_model``, ``coordinate_limit_min/max``,
+    ``integrator_accuracy``, ``model``), the state calls (``reset``,
+    ``set_time``, ``set_coordinates``, ``set_velocities``, ``actuate``,
+    ``integrate``), the realizations (``calc_joint_kinematics``,
+    ``calc_body_kinematics``, ``calc_muscles_info``, ``calc_forces_info``;
+    same dict keys) and ``save_simulation``.  Every call runs on the GPU
+    (``bioim_osim``); a realization is cached until the state changes.
+    Callers that drive the model directly (tests/example_position_control.py)
+    and the env methods (``get_state_dict``, ``get_limit_forces``,
+    ``calc_cost_of_transport``) use it."""
+
+    def __init__(self, env, names, action_min, action_max, index=0):
         self._env = env
-        self.step_size = float(env.pack.step_size)
+        self._i = int(index)
+        pk = env.pack
+        self._pack, self._names = pk, names
+        self.step_size = float(pk.step_size)
+        self.integrator_accuracy = float(env.integrator_accuracy)
         self.coordinate_names = list(names['coords'])
-        self.muscle_names = list(names['muscles']) if env.pack.nmuscle else []
-        self.is_muscle_model = env.pack.nmuscle > 0
+        self.muscle_names = list(names['muscles']) if pk.nmuscle else []
+        self.body_names = list(names['bodies'])
+        self.is_muscle_model = pk.nmuscle > 0
         self.action_min, self.action_max = list(action_min), list(action_max)
-        self.recorder = TrajectoryRecorder(env.pack, names)
+        self.action_space_size = len(self.action_min)
+        # opensim_wrapper.py:30-36: ranges of every coordinate but the pelvis translations
+        keep = [c for c, n in enumerate(self.coordinate_names) if n not in ('pelvis_tx', 'pelvis_ty', 'pelvis_tz')]
+        self.coordinate_limit_min = [float(pk.coord[c].range_min) for c in keep]
+        self.coordinate_limit_max = [float(pk.coord[c].range_max) for c in keep]
+        self.coordinate_names_multibody_order = self._multibody_order()
+        self.model = ModelView(pk, names)
+        self.recorder = TrajectoryRecorder(pk, names)
+        self.last_action = None
+        self._rep = None
+        self._obs = None
+
+    def _multibody_order(self):
+        """opensim_wrapper.py:74-90 restated: the key of a coordinate is its
+        mobilized body's index (ground 0, then the bodies in BodySet order; a
+        composite body's mobilized body is its first OpenSim body) plus an
+        offset — the running count, or the coordinate's q index within its
+        joint when that is not 0 (the count then advances)."""
+        pk, names = self._pack, self._names
+        first = {}
+        for b in range(pk.nosbody):
+            first.setdefault(int(pk.osbody[b].cbody), b)
+        joints = names.get('coord_joints') or [None] * len(self.coordinate_names)
+        keyed, cnt = {}, 0
+        for c, name in enumerate(self.coordinate_names):
+            mbix = first.get(int(pk.coord[c].cbody), -1) + 1
+            mqix = sum(1 for k in range(c) if joints[k] == joints[c])
+            offset = cnt
+            if mqix != 0:
+                offset = mqix
+                cnt += 1
+            keyed[mbix + offset] = name
+        return [keyed[k] for k in sorted(keyed)]
+
+    # ------------------------------------------------------------ state
+    def _dirty(self):
+        self._rep = None
+        self._obs = None
+
+    def _call(self, op, controls=None):
+        import torch
+        ctl = None if controls is None else torch.as_tensor(np.asarray(controls, dtype=np.float64).reshape(1, -1))
+        rep = self._env.osim(op, [self._i], controls=ctl, want_obs=True)
+        self._rep = split_osim_report(self._pack, rep[self._i].double().cpu().numpy())
+        self._obs = self._env.obs[self._i].double().cpu().numpy()
+        return self._rep
+
+    def report(self):
+        """the realized state (split_osim_report), realized on demand"""
+        if self._rep is None:
+            self._call('realize')
+        return self._rep
+
+    def observation(self):
+        """the env's observation row at the current state"""
+        if self._obs is None:
+            self._call('realize')
+        return self._obs
+
+    def _state(self):
+        return self._env.get_state()
+
+    def _set_state(self, s):
+        self._env.set_state(s)
+        self._dirty()
+
+    def _edit(self, fn):
+        """read-modify-write of this env's flat state row (include/bioim.h), then
+        reset_manager (a new integrator + equilibrateMuscles, :287-291)"""
+        s = self._state()
+        fn(s[self._i])
+        self._set_state(s)
+        self._call('equilibrate')
+        self.recorder.clear()       # the new Manager's state storage starts here (:336)
 
     @property
     def istep(self):
-        return int(self._env.get_state()[0, 1])
+        return int(self._state()[self._i, 1])
 
+    @property
+    def state(self):
+        """the flat state row (include/bioim.h layout) standing in for the SimTK::State"""
+        return self._state()[self._i]
+
+    def reset(self):
+        """opensim_wrapper.py:293-297: initializeState (defaults; the held
+        controls stay), time 0, istep 0, reset_manager"""
+        pk = self._pack
+        nd = pk.ndof
+
+        def f(s):
+            s[0] = 0.0
+            s[1] = 0
+            for c in range(pk.ncoord):
+                d = pk.coord[c].dof
+                if d >= 0:
+                    s[5 + d] = pk.coord[c].default_value
+                    s[5 + nd + d] = 0.0
+            for m in range(pk.nmuscle):
+                s[5 + 2 * nd + m] = pk.muscle[m].default_act
+        self._edit(f)
+
+    def set_time(self, t):
+        """opensim_wrapper.py:303-307 (istep = int(t / step_size), the float truncation kept)"""
+        def f(s):
+            s[0] = float(t)
+            s[1] = int(float(t) / self.step_size)
+        self._edit(f)
+
+    def _set_coords(self, values: dict, speeds: bool):
+        pk, nd = self._pack, self._pack.ndof
+
+        def f(s):
+            for name, v in values.items():
+                c = self.coordinate_names.index(name)
+                d = pk.coord[c].dof
+                if d >= 0:              # a locked coordinate ignores setValue
+                    s[5 + (nd if speeds else 0) + d] = float(v)
+        self._edit(f)
+
+    def set_coordinates(self, q_dict):
+        """opensim_wrapper.py:309-319"""
+        self._set_coords(q_dict, False)
+
+    def set_velocities(self, u_dict):
+        """opensim_wrapper.py:321-332"""
+        self._set_coords(u_dict, True)
+
+    def actuate(self, action):
+        """opensim_wrapper.py:92-107: NaN -> 0, clip, held as the controls"""
+        self._call('realize', controls=action)
+        pk, nd, nm, H, na = self._pack, self._pack.ndof, self._pack.nmuscle, self._pack.horizon, self._pack.nact
+        self.last_action = self._state()[self._i, 5 + 2 * nd + 2 * nm + H * na + na + 1:][:na].copy()
+
+    def get_last_action(self):
+        return self.last_action
+
+    def integrate(self):
+        """opensim_wrapper.py:299-301 with the handle's integrator"""
+        self._call('integrate')
+        self._record()
+
+    def _record(self):
+        r = self._rep
+        self.recorder.record(self._state()[self._i], r['qdd'], self._force_row(r))
+
+    @staticmethod
+    def _force_row(r):
+        return np.concatenate([r['actuation'], r['contact'].reshape(-1), r['limits']])
+
+    # ------------------------------------------------------------ realizations
+    def calc_joint_kinematics(self):
+        """opensim_wrapper.py:118-135"""
+        r = self.report()
+        obs = {'time': r['time'], 'coordinate_pos': {}, 'coordinate_vel': {}, 'coordinate_acc': {}}
+        for i, n in enumerate(self.coordinate_names):
+            obs['coordinate_pos'][n] = float(r['q'][i])
+            obs['coordinate_vel'][n] = float(r['u'][i])
+            obs['coordinate_acc'][n] = float(r['qdd'][i])
+        return obs
+
+    def calc_body_kinematics(self):
+        """opensim_wrapper.py:137-190: origins, body-fixed XYZ angles, ground-frame
+        velocities and accelerations per body; the system mass center"""
+        r = self.report()
+        obs = {'time': r['time']}
+        keys = ('body_pos', 'body_vel', 'body_acc', 'body_pos_rot', 'body_vel_rot', 'body_acc_rot')
+        for k in keys:
+            obs[k] = {}
+        for i, n in enumerate(self.body_names):
+            b = r['bodies'][i]
+            obs['body_pos'][n] = [float(x) for x in b[0:3]]
+            obs['body_vel'][n] = [float(x) for x in b[3:6]]
+            obs['body_acc'][n] = [float(x) for x in b[6:9]]
+            obs['body_pos_rot'][n] = [float(x) for x in b[9:12]]
+            obs['body_vel_rot'][n] = [float(x) for x in b[12:15]]
+            obs['body_acc_rot'][n] = [float(x) for x in b[15:18]]
+        c = r['com']
+        obs['body_pos']['center_of_mass'] = [float(x) for x in c[0:3]]
+        obs['body_vel']['center_of_mass'] = [float(x) for x in c[3:6]]
+        obs['body_acc']['center_of_mass'] = [float(x) for x in c[6:9]]
+        return obs
+
+    def calc_forces_info(self):
+        """opensim_wrapper.py:192-236: contact_forces = the negated ground-platform
+        record (the wrench on the feet), coordinate_limit_forces, and each
+        actuator's record value (its actuation) in scalar_actuator_forces"""
+        r = self.report()
+        obs = {'time': r['time'], 'forces': {}, 'contact_forces': {}, 'coordinate_limit_forces': {},
+               'scalar_actuator_forces': {}}
+        for i, n in enumerate(self._names['cforces']):
+            obs['contact_forces'][n] = [float(x) for x in r['contact'][i]]
+        for i, n in enumerate(self._names['limits']):
+            obs['coordinate_limit_forces'][n] = float(r['limits'][i])
+        anames = self.muscle_names if self.is_muscle_model else list(
+            self._names.get('actuators') or [f'{self.coordinate_names[self._pack.coordact[a].coord]}_actuator'
+                                              for a in range(self._pack.nact)])
+        for a, n in enumerate(anames):
+            obs['scalar_actuator_forces'][n] = float(r['actuation'][a])
+        return obs
+
+    def calc_muscles_info(self):
+        """opensim_wrapper.py:238-259"""
+        r = self.report()
+        obs = {'time': r['time']}
+        if self.is_muscle_model:
+            obs['muscles'] = {}
+            for i, n in enumerate(self.muscle_names):
+                m = r['muscles'][i]
+                obs['muscles'][n] = {'activation': float(m[0]), 'fiber_length': float(m[1]),
+                                     'fiber_velocity': float(m[2]), 'fiber_force': float(m[3])}
+        return obs
+
+    # ------------------------------------------------------------ fields
     def get_action_space_size(self):
-        return len(self.action_min)
+        return self.action_space_size
+
+    def get_coordinate_names(self):
+        return self.coordinate_names
+
+    def get_coordinate_names_multibody_order(self):
+        return self.coordinate_names_multibody_order
 
     def save_simulation(self, base_dir):
         """Writes simulation_States.sto, simulation_Kinematics_{q,u,dudt}.sto and

@@ -26,6 +26,7 @@ from . import _lib
 from .registry import load_pack
 
 INTEGRATORS = {'semi-implicit': 0, 'rk-merson': 1}
+OSIM_OPS = {'realize': 0, 'equilibrate': 1, 'integrate': 2}   # include/bioim.h BIOIM_OSIM_*
 
 
 def check_env_mask(mask, num_envs, device):
@@ -173,6 +174,31 @@ class VectorEnv:
         check_env_mask(mask, self.num_envs, self.device)
         self._active = mask
         _lib.check(self._L.bioim_set_active_mask(self._h, self._ptr(mask)))
+
+    def osim(self, op, env_ids, controls=None, want_obs=True):
+        """OsimModel calls on the listed envs (``bioim_osim``): optional
+        ``controls`` (n, nact) actuated first (NaN -> 0, clip, held), then op
+        'realize' (nothing else), 'equilibrate' (reset_manager: a new integrator
+        and the muscles' static fiber equilibrium at the held state) or
+        'integrate' (istep += 1, integrate to step_size * istep), then the
+        realize.  Returns the report rows (N, bioim_osim_report_dim) — rows of
+        the listed envs are fresh — and writes their obs rows into
+        ``self.obs`` when ``want_obs``."""
+        import torch
+        if getattr(self, 'osim_report', None) is None:
+            d = _lib.check(self._L.bioim_osim_report_dim(self._h))
+            self.osim_report = torch.zeros((self.num_envs, d), dtype=self.dtype, device=self.device)
+        ids = torch.as_tensor(env_ids, dtype=torch.int32, device=self.device).reshape(-1).contiguous()
+        if ids.numel() and (int(ids.min()) < 0 or int(ids.max()) >= self.num_envs):
+            raise ValueError(f'env ids must lie in [0, {self.num_envs})')
+        ctl = None
+        if controls is not None:
+            ctl = torch.as_tensor(controls, dtype=self.dtype, device=self.device).reshape(ids.numel(), self.action_dim)
+            ctl = ctl.contiguous()
+        self._bind_stream()
+        _lib.check(self._L.bioim_osim(self._h, OSIM_OPS[op], self._ptr(ids), ids.numel(), self._ptr(ctl),
+                                      self._ptr(self.obs) if want_obs else None, self._ptr(self.osim_report)))
+        return self.osim_report
 
     def pending_count(self) -> int:
         """Envs suspended mid-step by the RK budget."""

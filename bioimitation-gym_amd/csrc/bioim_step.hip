@@ -1504,10 +1504,9 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
                 muscle_path<T, Real>(SM, mu, lds, L, dLs);
                 STAMP(4);
                 Real a_ = act[j], l_ = lce[j];
-                if (equilibrate) { /* reset: default activation, static fiber equilibrium */
-                    a_ = mu.default_act;
+                if (equilibrate) /* equilibrateMuscles: static fiber equilibrium at the held activation
+                                  * (a reset has set the default activation) */
                     l_ = muscle_equilibrium<T, Real>(SM, mu, a_, L);
-                }
                 D.act[j] = a_;
                 D.lce[j] = l_;
                 /* the sphere contacts ride in the first muscle pass (every
@@ -1958,6 +1957,11 @@ template <class T, typename Real> struct LaunchArgs {
     uint8_t *ready_out; /* optional [N]: 1 where the env finished its step in this launch */
     const uint8_t *active; /* optional [N] (steps): 0 = no new action, the env is left untouched
                               unless it is finishing a suspended RK step */
+    /* mode 2 (OsimModel calls, REP kernels only; bioim_osim): op BIOIM_OSIM_*,
+     * optional controls [n_list][nact] actuated first, report rows [N][osim_dim] */
+    int osim_op, osim_dim;
+    const Real *controls_in;
+    Real *osim_out;
 };
 
 /* Reference integrator (RK kernels): OpenSim's Manager integrates with an
@@ -1988,10 +1992,173 @@ template <typename Real> DEV void rk_update(int s, Real h, Real f, Real &y, Real
     }
 }
 
+/* one muscle's term of calc_cost_of_transport (muscle_walking_imitation_env2D.py:360-403,
+ * Umberger-style heat and work rates): mass * (activation + maintenance heat)
+ * + shortening + work, from the excitation ex and the realized fiber state */
+template <typename Real> DEV Real muscle_cot(const SMuscle<Real> &mu, const MState<Real> &ms, Real ex) {
+    Real l = mu.slow, aa = ms.act, hp = Real(0.5 * 3.14159265358979323846);
+    Real se, ce, sa, ca;
+    sincos_rt(hp * ex, se, ce);
+    sincos_rt(hp * aa, sa, ca);
+    Real fa = Real(40) * l * se + Real(133) * (Real(1) - l) * (Real(1) - ce);
+    Real fm = Real(74) * l * sa + Real(111) * (Real(1) - l) * (Real(1) - ca);
+    Real ln = ms.lce * mu.inv_lopt, vv = ms.vce;
+    Real g = 0;
+    if (ln < Real(0.5)) g = Real(0.5);
+    else if (ln < Real(1)) g = ln;
+    else if (ln < Real(1.5)) g = Real(-2) * ln + Real(3);
+    Real es = fmax(Real(0), Real(0.25) * ms.Ff * -vv);
+    Real ew = fmax(Real(0), ms.Fa * -vv);
+    return mu.mass * fa + mu.mass * g * fm + es + ew;
+}
+
+/* OpenSim's body-fixed XYZ angles of R = Rx(a) Ry(b) Rz(c)
+ * (Rotation::convertRotationToBodyFixedXYZ, opensim_wrapper.py:164-167) */
+template <typename Real> DEV void body_fixed_xyz(const Real *R, Real *ang) {
+    ang[0] = atan2(-R[5], R[8]);
+    ang[1] = atan2(R[2], sqrt(R[0] * R[0] + R[1] * R[1]));
+    ang[2] = atan2(-R[1], R[0]);
+}
+
+/* The realized state as the OsimModel calc_* calls read it (REP kernels,
+ * bioim_osim; layout in include/bioim.h, BIOIM_OSIM_REPORT): time, istep;
+ * q, u, q'' (CoordinateSet order); per OpenSim body origin position,
+ * velocity, acceleration, body-fixed XYZ angles, angular velocity and
+ * acceleration (calc_body_kinematics, :137-190), then the system COM
+ * position, velocity, acceleration; per muscle activation, fiber length,
+ * fiber velocity, fiber force, active fiber force, excitation, tendon force
+ * (calc_muscles_info :238-259 and calc_cost_of_transport's getters); the
+ * actuation of each actuator; per Hunt-Crossley force the wrench on the feet
+ * about the ground origin (calc_forces_info :192-236); the limit forces;
+ * calc_cost_of_transport().  Reads the frames, accelerations, columns, q''
+ * and force slots the realize left in LDS; lane-parallel. */
+template <class T, typename Real>
+DEV void osim_report(const DModel<Real> &M, const SModel<T, Real> &SM, const Real *lds, int lane, const Dyn<T, Real> &D,
+                     const Real (&control)[Lay<T, Real>::MPL], double t, int istep, Real *out) {
+    using LY = Lay<T, Real>;
+    constexpr int G = T::G, NC = T::NC, ND = LY::ND, NOS = T::NOS, NM = T::NM, NA = T::NA, MPL = LY::MPL;
+    constexpr int CPL = (NC + G - 1) / G;
+    constexpr int OB = 2 + 3 * NC, OCOM = OB + 18 * NOS, OMU = OCOM + 9, OACT = OMU + 7 * NM, OCF = OACT + NA;
+    constexpr int OLIM = OCF + 6 * T::NF, OCOT = OLIM + T::NL;
+    const Real x0 = D.x0;
+    if (lane == 0) { out[0] = Real(t); out[1] = Real(istep); }
+#pragma unroll
+    for (int jc = 0; jc < CPL; ++jc) {
+        const int c = lane + jc * G;
+        if (c < NC) {
+            const int dc = SM.coord_dof[c];
+            out[2 + c] = lds[LY::QF + c];
+            out[2 + NC + c] = lds[LY::UF + c];
+            out[2 + 2 * NC + c] = dc >= 0 ? lds[LY::RHS + dc] : Real(0);
+        }
+    }
+    /* spatial acceleration of composite body cb (at the shifted ground
+     * origin): the velocity-product part plus its root path's columns x q'' */
+    auto body_acc = [&](int cb, Real *al, Real *aO) {
+        const Real *ab = lds + LY::AL + 6 * cb;
+        const uint32_t dm = SM.dofmask[cb];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { al[i] = ab[i]; aO[i] = ab[3 + i]; }
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+            const Real qdd = ((dm >> d) & 1u) ? lds[LY::RHS + d] : Real(0);
+            const Real *S = lds + LY::S + 6 * d;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { al[i] += S[i] * qdd; aO[i] += S[3 + i] * qdd; }
+        }
+    };
+    if (lane < NOS) {
+        const int cb = SM.os_cb[lane];
+        const Real *kb = lds + LY::KB + 18 * cb;
+        Real P[3], v[3], tt[3], al[3], aO[3], aP[3], Rb[9], ang[3];
+        mv3(kb, SM.os_p[lane], P);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) P[i] += kb[9 + i];
+        cross3(kb + 12, P, tt);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) v[i] = kb[15 + i] + tt[i];
+        body_acc(cb, al, aO);
+        Real t2[3];
+        cross3(al, P, tt);
+        cross3(kb + 12, v, t2);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) aP[i] = aO[i] + tt[i] + t2[i];
+        mm3(kb, M.os_R[lane], Rb);
+        body_fixed_xyz(Rb, ang);
+        Real *o = out + OB + 18 * lane;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            o[i] = P[i] + (i == 0 ? x0 : Real(0)); o[3 + i] = v[i]; o[6 + i] = aP[i];
+            o[9 + i] = ang[i]; o[12 + i] = kb[12 + i]; o[15 + i] = al[i];
+        }
+    } else if (lane == NOS) {
+        Real mt = 0, cs[3] = {0, 0, 0}, vs[3] = {0, 0, 0}, as[3] = {0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < T::NB; ++c) {
+            const Real *kb = lds + LY::KB + 18 * c;
+            Real cG[3], vc[3], ac[3], tt[3], t2[3], al[3], aO[3];
+            mv3(kb, SM.body[c].com, cG);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) cG[i] += kb[9 + i];
+            cross3(kb + 12, cG, tt);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) vc[i] = kb[15 + i] + tt[i];
+            body_acc(c, al, aO);
+            cross3(al, cG, tt);
+            cross3(kb + 12, vc, t2);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) ac[i] = aO[i] + tt[i] + t2[i];
+            const Real m = SM.body[c].mass;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { cs[i] += m * cG[i]; vs[i] += m * vc[i]; as[i] += m * ac[i]; }
+            mt += m;
+        }
+        Real *o = out + OCOM;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            o[i] = cs[i] / mt + (i == 0 ? x0 : Real(0)); o[3 + i] = vs[i] / mt; o[6 + i] = as[i] / mt;
+        }
+    }
+    Real cot = 0;
+#pragma unroll
+    for (int j = 0; j < MPL; ++j) {
+        const int m = mslot<T>(lane + j * G);
+        if constexpr (NM > 0) {
+            if (m < NM) {
+                const MState<Real> &ms = D.ms[j];
+                Real *o = out + OMU + 7 * m;
+                o[0] = ms.act; o[1] = ms.lce; o[2] = ms.vce; o[3] = ms.Ff; o[4] = ms.Fa; o[5] = control[j]; o[6] = ms.Ft;
+                cot += muscle_cot<Real>(SM.mus[m], ms, control[j]);
+            }
+        }
+        if (m < NA) {
+            if constexpr (NM > 0) out[OACT + m] = D.ms[j].Ft;
+            else out[OACT + m] = control[j] * SM.ca_opt[m];
+        }
+    }
+    if (lane < T::NF) {
+        Real F[3] = {0, 0, 0}, Mo[3] = {0, 0, 0};
+#pragma unroll
+        for (int s2 = 0; s2 < T::NS; ++s2) {
+            const Real *cw = lds + LY::CW + 8 * s2;
+            const bool mine = SM.sph_force[s2] == lane;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { F[i] += mine ? cw[i] : Real(0); Mo[i] += mine ? cw[3 + i] : Real(0); }
+        }
+        Mo[1] += -x0 * F[2];
+        Mo[2] += x0 * F[1];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { out[OCF + 6 * lane + i] = F[i]; out[OCF + 6 * lane + 3 + i] = Mo[i]; }
+    }
+    if (lane < T::NL) out[OLIM + lane] = lds[LY::LIM + 4 * lane];
+    cot = group_sum<G>(cot);
+    if (lane == 0) out[OCOT] = NM > 0 ? cot + Real(1.51) * M.total_mass : Real(0);
+}
+
 /* One 256-thread workgroup = 256/G envs of segment `a`, block `blk`.
  * RK: the reference integrator (adaptive Kutta-Merson) instead of the
  * fixed semi-implicit substeps. */
-template <class T, typename Real, bool PERT, bool RK>
+template <class T, typename Real, bool PERT, bool RK, bool REP>
 DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     using LY = Lay<T, Real>;
     constexpr int G = T::G, ND = LY::ND, NA = T::NA, NM = T::NM;
@@ -2001,6 +2168,8 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     const DModel<Real> *__restrict__ Mg = a.Mg;
     const DState<Real> &st = a.st;
     const int N = a.N, mode = a.mode;
+    /* mode 2 (OsimModel calls) exists in the REP kernels only */
+    const bool osim = REP && mode == 2;
     const Real *__restrict__ actions = a.actions;
     Real *__restrict__ obs = a.obs;
 #ifdef BIOIM_STAMPS
@@ -2024,7 +2193,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     int gidx = blk * EPB + slot;
     Real *lds = reinterpret_cast<Real *>(smem_raw + SMB) + slot * LY::SIZE;
     int env;
-    if (mode == 1) {
+    if (mode == 1 || osim) {
         if (gidx >= a.n_list) return;
         env = a.env_ids ? a.env_ids[gidx] : gidx;
         if (env < 0 || env >= N) return;
@@ -2058,6 +2227,10 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
 #pragma unroll
             for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
                 hist[j][hh] = hh < H ? st.hist[((size_t)hh * NA + m) * N + env] : Real(0);
+            /* held controls: the PrescribedController's Constant functions keep
+             * the last actuate() through OsimModel.reset (opensim_wrapper.py:92-107,
+             * :293-297), so a reset realizes with them */
+            if (mode != 0) control[j] = st.ctl[(size_t)m * N + env];
         }
     }
     int done = 0;
@@ -2084,7 +2257,54 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     const PertArgs<Real> PA{a.pert_x, a.pert_y, a.pert_n, a.pert_ob, env, N};
     double *pslot = reinterpret_cast<double *>(smem_raw + SMB + sizeof(Real) * EPB * LY::SIZE) + PERT_SLOT * slot;
     if (PERT && lane == 0) { pslot[0] = t; pslot[1] = 0; pslot[2] = 0; pslot[3] = -1; pslot[4] = 0; }
-    if (resume) {
+    /* OsimModel.integrate (opensim_wrapper.py:299-301): istep += 1, then
+     * integrate to the absolute time step_size * istep with the held controls */
+    auto begin_integrate = [&]() {
+        istep += 1;
+        double tf = M.step_size * (double)istep;
+        double hstep = tf - t;
+        if (hstep > 0) {
+            if constexpr (RK) {
+                rk_t = t; rk_tf = tf;
+                rk_h = rk_hnext > 0 ? rk_hnext : 1e-4;
+                remaining = 1;      /* integrating until rk_t reaches rk_tf */
+            } else {
+                dt = Real(hstep / (double)M.nsub);
+                remaining = M.nsub;
+                /* substep k starts at t + k * hstep / nsub (the oracle's substep times) */
+                if (PERT && lane == 0) { pslot[0] = t; pslot[1] = hstep / (double)M.nsub; }
+            }
+        }
+        t = tf;
+    };
+    bool eq_only = false;   /* mode 2 EQUILIBRATE: fiber equilibrium at the held state */
+    if (osim) {
+        if (a.controls_in) {
+            /* OsimModel.actuate (opensim_wrapper.py:92-107): NaN -> 0, clip */
+            Real raw[MPL];
+            bool nan_here = false;
+#pragma unroll
+            for (int j = 0; j < MPL; ++j) {
+                const int m = mslot<T>(lane + j * G);
+                raw[j] = m < NA ? a.controls_in[(size_t)gidx * NA + m] : Real(0);
+                nan_here = nan_here || (m < NA && isnan(raw[j]));
+            }
+            const bool anynan = group_any<G>(nan_here);
+#pragma unroll
+            for (int j = 0; j < MPL; ++j) {
+                const int m = mslot<T>(lane + j * G), ms = m < NA ? m : 0;
+                const Real lo = NM > 0 ? Real(0) : SM.ca_min[ms];
+                const Real hi = NM > 0 ? Real(1) : SM.ca_max[ms];
+                const Real v = anynan ? Real(0) : raw[j];
+                control[j] = m < NA ? (v < lo ? lo : (v > hi ? hi : v)) : Real(0);
+            }
+        }
+        if (a.osim_op == BIOIM_OSIM_INTEGRATE) begin_integrate();
+        if (a.osim_op == BIOIM_OSIM_EQUILIBRATE) {
+            eq_only = true;
+            rk_hnext = 0;   /* reset_manager: a new Manager / integrator (opensim_wrapper.py:287-291) */
+        }
+    } else if (resume) {
         /* the state is at the accepted RK point rk_t of the step ending at t */
 #pragma unroll
         for (int j = 0; j < MPL; ++j) {
@@ -2167,23 +2387,8 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             const Real v = pnan ? Real(0) : control[j];
             control[j] = m < NA ? (v < lo ? lo : (v > hi ? hi : v)) : Real(0);
         }
-        /* ---- integrate to step_size * istep (semi-implicit substeps) */
-        istep += 1;
-        double tf = M.step_size * (double)istep;
-        double hstep = tf - t;
-        if (hstep > 0) {
-            if constexpr (RK) {
-                rk_t = t; rk_tf = tf;
-                rk_h = rk_hnext > 0 ? rk_hnext : 1e-4;
-                remaining = 1;      /* integrating until rk_t reaches rk_tf */
-            } else {
-                dt = Real(hstep / (double)M.nsub);
-                remaining = M.nsub;
-                /* substep k starts at t + k * hstep / nsub (the oracle's substep times) */
-                if (PERT && lane == 0) { pslot[0] = t; pslot[1] = hstep / (double)M.nsub; }
-            }
-        }
-        t = tf;
+        /* ---- integrate to step_size * istep */
+        begin_integrate();
     }
 
     /* One dynamics call site (inlined once): the substeps, then the realize
@@ -2205,8 +2410,8 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             }
         }
         const bool sub = remaining > 0;
-        const bool eq = !sub && pending_reset;
-        if (eq) {
+        const bool eq = !sub && (pending_reset || eq_only);
+        if (!sub && pending_reset) {
             int r = clamp_row(reset_row, M.nrows);
             if (lane < ND) {
                 const int c = SM.dof_coord[lane];
@@ -2217,8 +2422,14 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             istep = M.ref_istep[r];
             has_last = 0;
             rk_hnext = 0;   /* reset_manager: a new integrator (opensim_wrapper.py:287-291) */
+            /* initializeState: the default activation (the held controls stay) */
+            if constexpr (NM > 0) {
 #pragma unroll
-            for (int j = 0; j < MPL; ++j) control[j] = 0;
+                for (int j = 0; j < MPL; ++j) {
+                    const int m = mslot<T>(lane + j * G);
+                    if (m < NM) act[j] = SM.mus[m].default_act;
+                }
+            }
             resets += 1;
         }
         {
@@ -2310,8 +2521,9 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                 for (int j = 0; j < MPL; ++j)
                     if (lane + j * G < NM) { act[j] = D.act[j]; lce[j] = D.lce[j]; }
             }
+            reported_reset = pending_reset;
             pending_reset = false;
-            reported_reset = true;
+            eq_only = false;
         }
         /* ---- realized state: observation (lane-parallel; get_state_dict,
          * muscle_walking_imitation_env2D.py:158-225).  The realize call left
@@ -2414,13 +2626,17 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             }
             if (lane < T::NL) fo[NA + 6 * T::NF + lane] = lds[LY::LIM + 4 * lane];
         }
+        if constexpr (REP) {
+            if (osim && a.osim_out)
+                osim_report<T, Real>(M, SM, lds, lane, D, control, t, istep, a.osim_out + (size_t)env * a.osim_dim);
+        }
         wave_sync();
         if (obs)
             for (int k = lane; k < M.obs_dim; k += G) obs[(size_t)env * a.obs_stride + k] = ob[k];
         if (a.final_obs && !reported_reset)
             for (int k = lane; k < M.obs_dim; k += G) a.final_obs[(size_t)env * a.obs_stride + k] = ob[k];
         wave_sync();
-        if (reported_reset) break;
+        if (reported_reset || osim) break;
 
         /* ---- reward (get_reward) and termination (is_done); group sums are
          * xor butterflies, so every lane holds bitwise-identical totals */
@@ -2471,21 +2687,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                     const int m = mslot<T>(lane + j * G);
                     if (m < NM) {
                         an += D.ms[j].act * D.ms[j].act;
-                        const SMuscle<Real> &mu = SM.mus[m];
-                        Real l = mu.slow, ex = control[j], aa = D.ms[j].act, hp = Real(0.5 * 3.14159265358979323846);
-                        Real se, ce, sa, ca;
-                        sincos_rt(hp * ex, se, ce);
-                        sincos_rt(hp * aa, sa, ca);
-                        Real fa = Real(40) * l * se + Real(133) * (Real(1) - l) * (Real(1) - ce);
-                        Real fm = Real(74) * l * sa + Real(111) * (Real(1) - l) * (Real(1) - ca);
-                        Real ln = D.ms[j].lce * mu.inv_lopt, vv = D.ms[j].vce;
-                        Real g = 0;
-                        if (ln < Real(0.5)) g = Real(0.5);
-                        else if (ln < Real(1)) g = ln;
-                        else if (ln < Real(1.5)) g = Real(-2) * ln + Real(3);
-                        Real es = fmax(Real(0), Real(0.25) * D.ms[j].Ff * -vv);
-                        Real ew = fmax(Real(0), D.ms[j].Fa * -vv);
-                        cot += mu.mass * fa + mu.mass * g * fm + es + ew;
+                        cot += muscle_cot<Real>(SM.mus[m], D.ms[j], control[j]);
                     }
                 }
                 a_error = exp(Real(-2) * sqrt(group_sum<G>(an)));
@@ -2552,20 +2754,29 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         st.istep[env] = istep;
         st.has_last[env] = has_last;
         st.old_px[env] = old_px;
-        st.done[env] = (mode == 0 && !do_reset && !suspend) ? done : 0;
+        if (!osim) st.done[env] = (mode == 0 && !do_reset && !suspend) ? done : 0;
         st.resets[env] = resets;
-        if (RK || mode == 1) st.hrk[env] = rk_hnext;
+        if (RK || mode == 1 || (osim && a.osim_op == BIOIM_OSIM_EQUILIBRATE)) st.hrk[env] = rk_hnext;
         if constexpr (RK) {
             st.pend[env] = suspend ? 1 : 0;
             if (suspend) { st.rkt[env] = rk_t; st.rkh[env] = rk_h; st.rka[env] = rk_attempts; a.done_out[env] = 0; }
             if (mode == 0 && a.ready_out) a.ready_out[env] = suspend ? 0 : 1;
         }
     }
+    /* the held controls (a step's actuate, or an OsimModel.actuate): kept
+     * through resets, read by resets and OsimModel calls */
+    if (mode == 0 || (osim && a.controls_in)) {
+#pragma unroll
+        for (int j = 0; j < MPL; ++j) {
+            const int m = mslot<T>(lane + j * G);
+            if (m < NA) st.ctl[(size_t)m * N + env] = control[j];
+        }
+    }
     if (RK && suspend) {
 #pragma unroll
         for (int j = 0; j < MPL; ++j) {
             const int m = mslot<T>(lane + j * G);
-            if (m < NA) { st.ctl[(size_t)m * N + env] = control[j]; st.cur[(size_t)m * N + env] = curr[j]; }
+            if (m < NA) st.cur[(size_t)m * N + env] = curr[j];
             if (NM > 0 && m < NM) st.vnw[(size_t)m * N + env] = D.ms[j].vN;
         }
     }
@@ -2583,9 +2794,12 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     }
 }
 
-template <class T, typename Real, bool PERT, bool RK>
+/* REP: the OsimModel-call kernels (mode 2, bioim_osim): the same code plus
+ * the full realize report; separate instantiations, so the step kernels are
+ * untouched by it */
+template <class T, typename Real, bool PERT, bool RK, bool REP = false>
 __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))) void env_kernel(LaunchArgs<T, Real> a) {
-    env_block<T, Real, PERT, RK>(a, blockIdx.x);
+    env_block<T, Real, PERT, RK, REP>(a, blockIdx.x);
 }
 
 
@@ -2972,12 +3186,18 @@ template <class T> bool topology_matches(const bioim_modelpack_t &p) {
 
 }  // namespace
 
+struct OsimCall {   /* mode 2 launch arguments (bioim_osim) */
+    int op;
+    const void *controls;
+    void *report;
+};
+
 struct Ops {
     int lanes;
     size_t lds_bytes;   /* per workgroup: model image + BIOIM_WG / lanes env regions */
     int (*upload)(bioim_handle_t *);
     void (*launch)(bioim_handle_t *, int mode, const void *actions, void *obs, void *reward, uint8_t *done, void *info,
-                   const int32_t *env_ids, const int32_t *ref_index, int n_list);
+                   const int32_t *env_ids, const int32_t *ref_index, int n_list, const OsimCall *oc);
     void (*id_launch)(bioim_handle_t *, int op, int n, const void *q, const void *u, const void *v, void *out);
 };
 
@@ -3014,12 +3234,18 @@ template <class T, typename Real, bool PERT = false> constexpr size_t lds_bytes(
            (PERT ? (size_t)(BIOIM_WG / T::G) * PERT_SLOT * sizeof(double) : 0);
 }
 
+/* bioim_osim_report_dim (include/bioim.h layout) */
+int osim_report_dim(const bioim_modelpack_t &p) {
+    return 2 + 3 * p.ncoord + 18 * p.nosbody + 9 + 7 * p.nmuscle + p.nact + 6 * p.ncforce + p.nlimit + 1;
+}
+
 template <class T, typename Real>
 LaunchArgs<T, Real> make_args(bioim_handle_t *h, int mode, const void *actions, void *obs, void *reward, uint8_t *done,
-                              void *info, const int32_t *env_ids, const int32_t *ref_index, int n_list) {
+                              void *info, const int32_t *env_ids, const int32_t *ref_index, int n_list,
+                              const OsimCall *oc) {
     constexpr int EPB = BIOIM_WG / T::G;
     LaunchArgs<T, Real> a;
-    const int count = mode == 1 ? n_list : h->n;
+    const int count = mode != 0 ? n_list : h->n;
     a.Mg = reinterpret_cast<const DModel<Real> *>(h->model);
     a.Sg = reinterpret_cast<const SModel<T, Real> *>(h->smodel);
     a.st = *reinterpret_cast<DState<Real> *>(h->dstate);
@@ -3040,21 +3266,32 @@ LaunchArgs<T, Real> make_args(bioim_handle_t *h, int mode, const void *actions, 
     a.pert_y = reinterpret_cast<const Real *>(h->pert_y);
     a.pert_n = h->pert_n; a.pert_ob = h->pert_ob;
     a.rk_acc = h->rk_acc;
-    a.rk_budget = h->rk ? h->rk_budget : 0;
+    a.rk_budget = h->rk && mode == 0 ? h->rk_budget : 0;   /* an OsimModel integrate finishes its step */
     a.ready_out = mode == 0 ? h->ready_out : nullptr;
     a.active = mode == 0 ? h->active : nullptr;
+    a.osim_op = oc ? oc->op : 0;
+    a.osim_dim = osim_report_dim(h->pack);
+    a.controls_in = oc ? reinterpret_cast<const Real *>(oc->controls) : nullptr;
+    a.osim_out = oc ? reinterpret_cast<Real *>(oc->report) : nullptr;
     return a;
 }
 
 template <class T, typename Real>
 void launch_impl(bioim_handle_t *h, int mode, const void *actions, void *obs, void *reward, uint8_t *done, void *info,
-                 const int32_t *env_ids, const int32_t *ref_index, int n_list) {
-    LaunchArgs<T, Real> a = make_args<T, Real>(h, mode, actions, obs, reward, done, info, env_ids, ref_index, n_list);
+                 const int32_t *env_ids, const int32_t *ref_index, int n_list, const OsimCall *oc) {
+    LaunchArgs<T, Real> a = make_args<T, Real>(h, mode, actions, obs, reward, done, info, env_ids, ref_index, n_list, oc);
     if (a.blocks <= 0) return;
     /* the perturbation kernels are separate instantiations, so the default
      * kernels' code is untouched by the (rarely used) push */
     constexpr size_t lds0 = lds_bytes<T, Real, false>(), lds1 = lds_bytes<T, Real, true>();
     const dim3 g(a.blocks), b(BIOIM_WG);
+    if (mode == 2) {   /* OsimModel calls: the REP kernels */
+        if (a.pert_n > 0 && h->rk) hipLaunchKernelGGL((env_kernel<T, Real, true, true, true>), g, b, lds1, h->stream, a);
+        else if (a.pert_n > 0) hipLaunchKernelGGL((env_kernel<T, Real, true, false, true>), g, b, lds1, h->stream, a);
+        else if (h->rk) hipLaunchKernelGGL((env_kernel<T, Real, false, true, true>), g, b, lds0, h->stream, a);
+        else hipLaunchKernelGGL((env_kernel<T, Real, false, false, true>), g, b, lds0, h->stream, a);
+        return;
+    }
     if (a.pert_n > 0 && h->rk) hipLaunchKernelGGL((env_kernel<T, Real, true, true>), g, b, lds1, h->stream, a);
     else if (a.pert_n > 0) hipLaunchKernelGGL((env_kernel<T, Real, true, false>), g, b, lds1, h->stream, a);
     else if (h->rk) hipLaunchKernelGGL((env_kernel<T, Real, false, true>), g, b, lds0, h->stream, a);
@@ -3083,6 +3320,14 @@ template <class T, typename Real> int upload_smodel(bioim_handle_t *h) {
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, false, true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, false>()));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, true, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, true>()));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, false, false, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, false>()));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, true, false, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, true>()));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, false, true, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, false>()));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel<T, Real, true, true, true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, true>()));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&id_kernel<T, Real>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, Real, false>()));
@@ -3189,6 +3434,7 @@ template <typename Real> int xfer_state(bioim_handle_t *h, double *host, const d
                 for (int i = 0; i < na; ++i) s[k++] = hs.hist[(hh * na + i) * n + e];
             for (int i = 0; i < na; ++i) s[k++] = hs.last[i * n + e];
             s[k++] = hs.hrk[e];
+            for (int i = 0; i < na; ++i) s[k++] = hs.ctl[i * n + e];
         } else {
             const double *s = in + e * dim;
             int k = 0;
@@ -3202,6 +3448,7 @@ template <typename Real> int xfer_state(bioim_handle_t *h, double *host, const d
                 for (int i = 0; i < na; ++i) hs.hist[(hh * na + i) * n + e] = (Real)s[k++];
             for (int i = 0; i < na; ++i) hs.last[i * n + e] = (Real)s[k++];
             hs.hrk[e] = s[k++];
+            for (int i = 0; i < na; ++i) hs.ctl[i * n + e] = (Real)s[k++];
             hs.pend[e] = 0;   /* a state set from outside is at a step boundary */
         }
     }
@@ -3313,7 +3560,7 @@ int bioim_reset(bioim_handle_t *h, const int32_t *env_ids, const int32_t *ref_in
     int count = env_ids ? n : h->n;
     if (count <= 0) return 0;
     HIPCHK(hipSetDevice(h->device));
-    h->ops.launch(h, 1, nullptr, obs, nullptr, nullptr, nullptr, env_ids, ref_index, count);
+    h->ops.launch(h, 1, nullptr, obs, nullptr, nullptr, nullptr, env_ids, ref_index, count, nullptr);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -3321,7 +3568,7 @@ int bioim_reset(bioim_handle_t *h, const int32_t *env_ids, const int32_t *ref_in
 int bioim_step(bioim_handle_t *h, const void *actions, void *obs, void *reward, uint8_t *done, void *info) {
     if (!h || !actions || !done) return fail(BIOIM_E_ARG, "bioim_step: null handle/actions/done");
     HIPCHK(hipSetDevice(h->device));
-    h->ops.launch(h, 0, actions, obs, reward, done, info, nullptr, nullptr, 0);
+    h->ops.launch(h, 0, actions, obs, reward, done, info, nullptr, nullptr, 0, nullptr);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -3439,7 +3686,7 @@ int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs
         h->ops.launch(h, 0, (const char *)actions + off * h->act_stride * R,
                       obs ? (char *)obs + off * h->obs_stride * R : nullptr,
                       reward ? (char *)reward + off * R : nullptr, done + off,
-                      info ? (char *)info + off * h->info_stride * R : nullptr, nullptr, nullptr, 0);
+                      info ? (char *)info + off * h->info_stride * R : nullptr, nullptr, nullptr, 0, nullptr);
         h->stream = own;
         if (i > 0) {
             HIPCHK(hipEventRecord(h->ev_join, h->side));
@@ -3494,6 +3741,25 @@ int bioim_id_eval(bioim_handle_t *h, int op, int n, const void *q, const void *u
     return 0;
 }
 
+int bioim_osim_report_dim(const bioim_handle_t *h) {
+    if (!h) return fail(BIOIM_E_ARG, "null handle");
+    return osim_report_dim(h->pack);
+}
+
+int bioim_osim(bioim_handle_t *h, int op, const int32_t *env_ids, int n, const void *controls, void *obs, void *report) {
+    if (!h || op < BIOIM_OSIM_REALIZE || op > BIOIM_OSIM_INTEGRATE || n < 0 || (n > 0 && !env_ids))
+        return fail(BIOIM_E_ARG, "bioim_osim: bad arguments");
+    if (n == 0) return 0;
+    const int np = bioim_pending_count(h);
+    if (np < 0) return np;
+    if (np > 0) return fail(BIOIM_E_ARG, "bioim_osim: envs are suspended mid-step (bioim_set_rk_budget)");
+    HIPCHK(hipSetDevice(h->device));
+    const OsimCall oc{op, controls, report};
+    h->ops.launch(h, 2, nullptr, obs, nullptr, nullptr, nullptr, env_ids, nullptr, n, &oc);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 int bioim_set_env_offset(bioim_handle_t *h, int offset) {
     if (!h || offset < 0) return fail(BIOIM_E_ARG, "bioim_set_env_offset: bad arguments");
     h->env_offset = offset;
@@ -3502,7 +3768,7 @@ int bioim_set_env_offset(bioim_handle_t *h, int offset) {
 
 int bioim_state_dim(const bioim_handle_t *h) {
     if (!h) return fail(BIOIM_E_ARG, "null handle");
-    return 5 + 2 * h->ndof + 2 * h->nmuscle + h->horizon * h->nact + h->nact + 1;
+    return 5 + 2 * h->ndof + 2 * h->nmuscle + h->horizon * h->nact + h->nact + 1 + h->nact;
 }
 
 int bioim_get_state(bioim_handle_t *h, double *host_state) {

@@ -40,7 +40,9 @@
  * Flat per-env state (bioim_get_state/set_state, doubles), matching the
  * oracle's layout: [t, istep, has_last, old_pelvis_x, done, q[ndof], u[ndof],
  * activation[nmuscle], fiber_length[nmuscle], hist[horizon][nact],
- * last_action[nact]].
+ * last_action[nact], rk_step_size, controls[nact]] — controls are the held
+ * actuator controls (the PrescribedController's Constant functions, set by
+ * each step's actuate and kept through resets).
  */
 #ifndef BIOIM_H
 #define BIOIM_H
@@ -127,6 +129,44 @@ enum {
     BIOIM_ID_TOTAL = 5,
 };
 int bioim_id_eval(bioim_handle_t *h, int op, int n, const void *q, const void *u, const void *v, void *out);
+/* OsimModel calls on single envs (the reference's physics facade,
+ * opensim_wrapper.py:92-332), for callers that drive the model directly
+ * (tests/example_position_control.py:203-223; the env methods
+ * get_state_dict / get_limit_forces / calc_cost_of_transport).  For the n
+ * listed envs (env_ids: device int32[n]):
+ *   controls (device [n][nact], may be NULL): OsimModel.actuate first —
+ *     NaN -> 0, clip to [min_control, max_control], held from then on;
+ *   op BIOIM_OSIM_REALIZE: nothing else (the calc_* realizations);
+ *   op BIOIM_OSIM_EQUILIBRATE: reset_manager (:287-291) — a new integrator
+ *     and equilibrateMuscles: each muscle's static fiber equilibrium at the
+ *     held activation; the caller writes time / coordinates / speeds with
+ *     bioim_set_state first (set_time :303-307, set_coordinates :309-319,
+ *     set_velocities :321-332, reset :293-297);
+ *   op BIOIM_OSIM_INTEGRATE: integrate (:299-301) — istep += 1, then the
+ *     handle's integrator to step_size * istep with the held controls;
+ * then the state is realized: obs (device [N][obs_stride], may be NULL)
+ * gets the env's observation row, report (device [N][bioim_osim_report_dim],
+ * may be NULL) the realized quantities (rows indexed by env):
+ *   [time, istep, q[nc], u[nc], qdd[nc] (CoordinateSet order),
+ *    per OpenSim body: origin pos[3], vel[3], acc[3], body-fixed XYZ angles[3],
+ *      angular vel[3], angular acc[3] (ground frame); then the system COM
+ *      pos[3], vel[3], acc[3],
+ *    per muscle: activation, fiber_length, fiber_velocity, fiber_force,
+ *      active_fiber_force, excitation, tendon_force,
+ *    per actuator: actuation,
+ *    per Hunt-Crossley force: force[3], moment about the ground origin[3] on the feet,
+ *    per CoordinateLimitForce: its generalized force,
+ *    calc_cost_of_transport() (0 for torque models)].
+ * Env-level state (action deque, last action, old pelvis x, done) is left
+ * alone.  Refused while envs are suspended mid-step (bioim_set_rk_budget).
+ * Asynchronous on the handle's stream. */
+enum {
+    BIOIM_OSIM_REALIZE = 0,
+    BIOIM_OSIM_EQUILIBRATE = 1,
+    BIOIM_OSIM_INTEGRATE = 2,
+};
+int bioim_osim_report_dim(const bioim_handle_t *h);
+int bioim_osim(bioim_handle_t *h, int op, const int32_t *env_ids, int n, const void *controls, void *obs, void *report);
 /* Global index of this handle's env 0 (multi-GPU sharding): device-drawn
  * reset indices depend on the global env index, so a sharded run is
  * bit-identical to an unsharded one. */

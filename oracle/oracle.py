@@ -53,6 +53,15 @@ class Oracle:
             ('orc_env_set_integrator', C.c_int, [C.c_void_p, C.c_int, C.c_double]),
             ('orc_env_rk_stats', None, [C.c_void_p, _dp]),
             ('orc_force_report', C.c_int, [C.c_void_p, C.c_void_p, _dp]),
+            ('orc_osim_reset', None, [C.c_void_p, C.c_void_p]),
+            ('orc_osim_set_time', None, [C.c_void_p, C.c_void_p, C.c_double]),
+            ('orc_osim_set_coords', None, [C.c_void_p, C.c_void_p, _dp, C.c_int]),
+            ('orc_osim_actuate', None, [C.c_void_p, C.c_void_p, _dp]),
+            ('orc_osim_integrate', None, [C.c_void_p, C.c_void_p]),
+            ('orc_osim_reset_manager', None, [C.c_void_p, C.c_void_p]),
+            ('orc_osim_full_report_dim', C.c_int, [C.c_void_p]),
+            ('orc_osim_full_report', None, [C.c_void_p, C.c_void_p, _dp]),
+            ('orc_env_observe', None, [C.c_void_p, C.c_void_p, _dp]),
         ]:
             f = getattr(L, name)
             f.restype = res
@@ -115,6 +124,41 @@ class Oracle:
         out = np.zeros(pk.nact + 6 * pk.ncforce + pk.nlimit)
         self.lib.orc_force_report(self.pk, self.env_ptr(envs, i), _ptr(out))
         return out
+
+    # ------------------------------------------------------------ OsimModel calls
+    # (opensim_wrapper.py:92-332 restated; the HIP path's bioim_osim)
+    def osim_reset(self, envs, i):
+        self.lib.orc_osim_reset(self.pk, self.env_ptr(envs, i))
+
+    def osim_set_time(self, envs, i, t):
+        self.lib.orc_osim_set_time(self.pk, self.env_ptr(envs, i), float(t))
+
+    def osim_set_coords(self, envs, i, qfull, speeds=False):
+        """all coordinates in CoordinateSet order (locked ones are ignored)"""
+        v = np.ascontiguousarray(qfull, dtype=np.float64)
+        self.lib.orc_osim_set_coords(self.pk, self.env_ptr(envs, i), _ptr(v), int(bool(speeds)))
+
+    def osim_actuate(self, envs, i, action):
+        a = np.ascontiguousarray(action, dtype=np.float64)
+        self.lib.orc_osim_actuate(self.pk, self.env_ptr(envs, i), _ptr(a))
+
+    def osim_integrate(self, envs, i):
+        self.lib.orc_osim_integrate(self.pk, self.env_ptr(envs, i))
+
+    def osim_reset_manager(self, envs, i):
+        self.lib.orc_osim_reset_manager(self.pk, self.env_ptr(envs, i))
+
+    def osim_report(self, envs, i):
+        """the realized state of env i, include/bioim.h bioim_osim report layout"""
+        out = np.zeros(self.lib.orc_osim_full_report_dim(self.pk))
+        self.lib.orc_osim_full_report(self.pk, self.env_ptr(envs, i), _ptr(out))
+        return out
+
+    def observe(self, envs, i):
+        """env i's observation at its current state"""
+        obs = np.zeros(self.pack.obs_dim)
+        self.lib.orc_env_observe(self.pk, self.env_ptr(envs, i), _ptr(obs))
+        return obs
 
     def state_dim(self):
         return self.lib.orc_state_dim(self.pk)

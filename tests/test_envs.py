@@ -75,7 +75,7 @@ def test_trajectory_recorder_writes_opensim_storage(tmp_path):
     pk, names = load_pack(env_id), load_names(env_id)
     rec = TrajectoryRecorder(pk, names)
     rng = np.random.default_rng(0)
-    dim = 5 + 2 * pk.ndof + 2 * pk.nmuscle + pk.horizon * pk.nact + pk.nact + 1
+    dim = 5 + 2 * pk.ndof + 2 * pk.nmuscle + pk.horizon * pk.nact + pk.nact + 1 + pk.nact
     rows = []
     for k in range(4):
         s = rng.normal(size=dim)

@@ -1,0 +1,230 @@
+"""OsimModel calls on the HIP path (bioim_osim, include/bioim.h) and the
+task envs' public methods, against the fp64 oracle's OsimModel restatement
+(orc_osim_*, orc_osim_full_report).
+
+Tolerance: fp64 on both sides, same algorithm; 1e-9 relative to
+max(|x|, 1) for every report entry (the step-parity bound of
+tests/test_gpu_parity.py uses 1e-6 and observes ~1e-9).  The report's
+accelerations (q'', body and COM accelerations) carry the conditioning of
+q'' itself; observed at the rounding level in the step tests.
+"""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason='needs a HIP GPU')]
+
+IDS = ['MuscleWalkingImitation2D-v0', 'TorqueWalkingImitation2D-v0', 'MuscleRunningImitation3D-v0',
+       'MuscleLockedKneeImitation3D-v0', 'MusclePalsyImitation3D-v0', 'TorqueWalkingImitation3D-v0',
+       'TorqueLockedKneeImitation2D-v0']
+
+
+def _rel(a, b):
+    return np.abs(a - b) / np.maximum(1.0, np.abs(b))
+
+
+def _acts(pk, rng, n, rows):
+    if pk.nmuscle:
+        return rng.uniform(0.0, 1.0, size=(n, pk.nact))
+    base = np.array([[pk.ref_q[min(int(r), pk.nrows - 1)][pk.pd_coord[i]] for i in range(pk.nact)] for r in rows])
+    return base + rng.normal(0.0, 0.05, size=(n, pk.nact))
+
+
+def _pair(env_id, n, integrator='semi-implicit'):
+    import oracle
+    from bioimitation.registry import load_pack
+    from bioimitation.vector_env import VectorEnv
+    pk = load_pack(env_id)
+    env = VectorEnv(env_id, n, config={'integrator': integrator}, precision=64)
+    orc = oracle.Oracle(pk)
+    bufs = orc.new_envs(n)
+    for i in range(n):
+        orc.set_integrator(bufs, i, 'euler' if integrator == 'semi-implicit' else 'rk-merson', 1e-3)
+    return pk, env, orc, bufs
+
+
+@pytest.mark.parametrize('env_id', IDS)
+def test_realize_report_matches_oracle(env_id):
+    """After reset + 6 free-running steps (held controls from the last step),
+    the realize report of every env — q/u/q'', every body's origin
+    position/velocity/acceleration, body-fixed angles, angular velocity and
+    acceleration, COM, muscle states and forces, actuation, contact wrenches,
+    limit forces, cost of transport — equals the oracle's; so does the
+    observation written by the same call."""
+    import torch
+    n = 24
+    rng = np.random.default_rng(5)
+    pk, env, orc, bufs = _pair(env_id, n)
+    rows = rng.integers(0, pk.reset_hi + 1, size=n)
+    env.reset(ref_index=rows)
+    for i in range(n):
+        orc.reset(bufs, i, int(rows[i]))
+    for t in range(6):
+        a = _acts(pk, rng, n, rows + t + 1)
+        env.step(torch.as_tensor(a, device=env.device))
+        for i in range(n):
+            orc.step(bufs, i, a[i])
+    rep = env.osim('realize', np.arange(n)).cpu().numpy()
+    obs = env.obs.cpu().numpy()
+    worst = 0.0
+    for i in range(n):
+        want = orc.osim_report(bufs, i)
+        e = _rel(rep[i], want)
+        assert e.max() < 1e-9, (i, int(np.argmax(e)), e.max())
+        np.testing.assert_allclose(obs[i], orc.observe(bufs, i), rtol=1e-9, atol=1e-9)
+        worst = max(worst, e.max())
+    print(f'{env_id}: realize report max rel err {worst:.2e} over {n} envs')
+    env.close()
+
+
+@pytest.mark.parametrize('env_id', ['MuscleWalkingImitation2D-v0', 'TorqueWalkingImitation2D-v0',
+                                    'MuscleRunningImitation3D-v0', 'MuscleLockedKneeImitation3D-v0'])
+def test_reference_reset_body_through_facade_matches_bioim_reset(env_id):
+    """The reference's own reset body (muscle_walking_imitation_env2D.py:133-156)
+    run through the env's OsimModel facade on the GPU — osim_model.reset(),
+    set_time(q_d.time[index]), set_coordinates(q_d row), set_velocities(u_d
+    row), then get_observation() — gives bioim_reset's state and
+    observation at that row."""
+    from bioimitation import envs
+    from bioimitation.vector_env import VectorEnv
+    env = envs.make(env_id)
+    env.reset()
+    pk = env._env.pack
+    om = env.osim_model
+    names = om.coordinate_names
+    ref = VectorEnv(env_id, 1, precision=64)
+    for index in (0, 29, 58, pk.reset_hi):
+        om.reset()
+        om.set_time(pk.ref_time[index])
+        om.set_coordinates({n: pk.ref_q[index][c] for c, n in enumerate(names)})
+        om.set_velocities({n: pk.ref_u[index][c] for c, n in enumerate(names)})
+        obs = np.array(env.get_observation())
+        want = ref.reset(env_ids=[0], ref_index=[index])[0].cpu().numpy()
+        np.testing.assert_allclose(obs, want, rtol=1e-12, atol=1e-12)
+        s, w = env._env.get_state()[0], ref.get_state()[0]
+        sl = 5 + 2 * pk.ndof + 2 * pk.nmuscle
+        keep = np.ones(sl, bool)
+        keep[2] = keep[4] = False     # has_last / done: env-level, cleared by the env's reset only
+        np.testing.assert_allclose(s[:sl][keep], w[:sl][keep], rtol=1e-12, atol=1e-12)
+        assert om.istep == pk.ref_istep[index]
+    ref.close()
+    env.close()
+
+
+@pytest.mark.parametrize('env_id,integrator', [('TorqueWalkingImitation2D-v0', 'semi-implicit'),
+                                               ('MuscleWalkingImitation2D-v0', 'semi-implicit'),
+                                               ('MuscleRunningImitation3D-v0', 'rk-merson'),
+                                               ('TorqueWalkingImitation3D-v0', 'rk-merson')])
+def test_facade_actuate_integrate_matches_oracle(env_id, integrator):
+    """OsimEnv.step's physics half driven through the facade
+    (opensim_environment.py:100-102: actuate, integrate) for 8 steps, with
+    the handle's integrator, against the oracle's orc_osim_actuate /
+    orc_osim_integrate: reports to 1e-9, and get_last_action is the clipped
+    action."""
+    from bioimitation import envs
+    env = envs.make(env_id, config={'integrator': integrator})
+    env.reset()
+    pk = env._env.pack
+    om = env.osim_model
+    import oracle
+    orc = oracle.Oracle(pk)
+    bufs = orc.new_envs(1)
+    orc.set_integrator(bufs, 0, 'euler' if integrator == 'semi-implicit' else 'rk-merson', 1e-3)
+    orc.set_state(bufs, 0, env._env.get_state()[0])
+    rng = np.random.default_rng(9)
+    for t in range(8):
+        r = om.istep + 1
+        if pk.nmuscle:
+            a = rng.uniform(-0.2, 1.2, size=pk.nact)
+        else:   # torques around the PD law's magnitude
+            a = rng.normal(0.0, 60.0, size=pk.nact)
+        om.actuate(a)
+        np.testing.assert_allclose(om.get_last_action(), np.clip(a, om.action_min, om.action_max), rtol=0, atol=0)
+        om.integrate()
+        orc.osim_actuate(bufs, 0, a)
+        orc.osim_integrate(bufs, 0)
+        e = _rel(np.concatenate([[om.report()['time'], om.report()['istep']]]), orc.osim_report(bufs, 0)[:2])
+        assert e.max() == 0.0
+        want = orc.osim_report(bufs, 0)
+        from bioimitation.simulation_io import split_osim_report
+        got = env._env.osim_report[0].cpu().numpy()
+        err = _rel(got, want)
+        assert err.max() < 1e-9, (t, int(np.argmax(err)), err.max())
+        assert om.istep == r
+        assert split_osim_report(pk, got)['istep'] == r
+    assert len(om.recorder.rows) == 8
+    env.close()
+
+
+@pytest.mark.parametrize('env_id', ['TorqueWalkingImitation2D-v0', 'TorqueWalkingImitation3D-v0'])
+def test_held_controls_survive_reset(env_id):
+    """OsimModel.reset re-initializes the state, not the PrescribedController's
+    Constant functions (opensim_wrapper.py:38-56, 92-107, 293-297): after
+    some steps, a reset realizes with the last step's controls — the torque
+    models' reset q'' shows them.  Explicit resets (bioim_reset) and in-kernel
+    auto-resets both match the oracle, which holds them too."""
+    import torch
+    n = 32
+    rng = np.random.default_rng(3)
+    pk, env, orc, bufs = _pair(env_id, n)
+    rows = rng.integers(0, pk.reset_hi + 1, size=n)
+    env.reset(ref_index=rows)
+    for i in range(n):
+        orc.reset(bufs, i, int(rows[i]))
+    for t in range(3):
+        a = _acts(pk, rng, n, rows + t + 1)
+        env.step(torch.as_tensor(a, device=env.device))
+        for i in range(n):
+            orc.step(bufs, i, a[i])
+    rows2 = rng.integers(0, pk.reset_hi + 1, size=n)
+    obs = env.reset(ref_index=rows2).cpu().numpy()
+    want = np.stack([orc.reset(bufs, i, int(rows2[i])) for i in range(n)])
+    np.testing.assert_allclose(obs, want, rtol=1e-9, atol=1e-9)
+    # the same rows with zero held controls differ in q'' (the effect is real)
+    fresh = orc.new_envs(1)
+    z = orc.reset(fresh, 0, int(rows2[0]))
+    assert np.abs(z - want[0]).max() > 1e-3
+    st = env.get_state()
+    for i in range(n):
+        np.testing.assert_allclose(st[i], orc.get_state(bufs, i), rtol=1e-9, atol=1e-9)
+    env.close()
+
+
+def test_env_public_methods():
+    """get_state_dict / get_observation / get_observation_dict / get_reward /
+    is_done / get_limit_forces / calc_cost_of_transport / get_mass /
+    get_height / get_gravity (muscle_walking_imitation_env2D.py:102-403,
+    opensim_environment.py:52-98) on the single-env API: the observation dict
+    is the step's observation, state_dict holds the calc_* dicts, the cost of
+    transport equals the oracle's at that state, the limit forces the report's."""
+    from bioimitation import envs
+    import oracle
+    env_id = 'MuscleWalkingImitation2D-v0'
+    env = envs.make(env_id)
+    env.reset()
+    rng = np.random.default_rng(1)
+    for _ in range(4):
+        o, r, d, info = env.step(rng.uniform(0, 1, size=14))
+    assert env.get_reward() == (r, info['all_rewards']) and env.is_done() == d
+    np.testing.assert_array_equal(np.array(env.get_observation()), o)
+    sd = env.get_state_dict()
+    assert sd == env.get_observation_dict()
+    assert set(env.state_dict) >= {'coordinate_pos', 'body_pos', 'body_acc', 'body_pos_rot', 'muscles',
+                                   'contact_forces', 'coordinate_limit_forces', 'scalar_actuator_forces'}
+    pk = env._env.pack
+    orc = oracle.Oracle(pk)
+    bufs = orc.new_envs(1)
+    orc.set_state(bufs, 0, env._env.get_state()[0])
+    want = orc.osim_report(bufs, 0)
+    assert abs(env.calc_cost_of_transport() - want[-1]) <= 1e-9 * abs(want[-1])
+    lim = want[-1 - pk.nlimit:-1]
+    np.testing.assert_allclose(env.get_limit_forces(), lim, rtol=1e-9, atol=1e-9)
+    assert env.get_mass() == pytest.approx(75.1646, abs=1e-3) and env.get_height() == 1.80
+    assert env.get_gravity()[1] == pytest.approx(-9.80665)
+    env.close()
+    tenv = envs.make('TorqueWalkingImitation2D-v0')
+    tenv.reset()
+    with pytest.raises(AttributeError):
+        tenv.calc_cost_of_transport()
+    tenv.close()
