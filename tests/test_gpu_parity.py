@@ -503,7 +503,9 @@ def test_rk_merson_parity_fp64(env_id):
             errs.append(e)
             qerr = max(qerr, _rel(obs[i], o)[qdd].max())
             s = orc.get_state(bufs, i)
-            serr = max(serr, _rel(gst[i, 5:-1], s[5:-1]).max())
+            hrk = 5 + 2 * pk.ndof + 2 * pk.nmuscle + (pk.horizon + 1) * pk.nact   # the carried step size
+            keep = np.arange(len(s)) != hrk
+            serr = max(serr, _rel(gst[i, 5:][keep[5:]], s[5:][keep[5:]]).max())
             assert bool(done[i]) == d or e > 1e-8, (t, i)
             if d:
                 orc.reset(bufs, i, int(rng.integers(0, 120)))
@@ -556,7 +558,7 @@ def test_parity_200_steps_3d_envs_kept_up(env_id):
     what the HIP path must do is not diverge faster than that.  Bounds: obs
     and reward within 1e-4 relative (north_star) and equal `done` for the
     first 60 steps; afterwards, on envs alive on both sides, GPU-vs-oracle
-    error at most 1e4 x the twin's (or 1e-4); >= 50 % of the GPU's envs alive
+    error at most 100 x the twin's (or 1e-4); >= 50 % of the GPU's envs alive
     at t = 200.  Actions come from the oracle's state and go to all sides."""
     import torch
     n, T, cfg = 32, 200, {'horizon': 1}
@@ -591,6 +593,66 @@ def test_parity_200_steps_3d_envs_kept_up(env_id):
     ks = [0, 24, 49, 84, 99, 149, 199]
     print(f'{env_id} 200 steps, tracking drive: GPU alive at t=200 {gpu_alive.sum()}/{n}; max rel err GPU vs oracle / '
           f'oracle vs its one-ulp twin at t=' + ', '.join(f'{k + 1}: {e_gpu[k]:.1e} / {e_twin[k]:.1e}' for k in ks))
-    assert (e_gpu[60:] <= np.maximum(1e-4, 1e4 * e_twin[60:])).all(), np.argmax(e_gpu[60:] / np.maximum(1e-30, e_twin[60:]))
+    assert (e_gpu[60:] <= np.maximum(1e-4, 100 * e_twin[60:])).all(), np.argmax(e_gpu[60:] / np.maximum(1e-30, e_twin[60:]))
     assert gpu_alive.sum() >= n // 2
+    env.close()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+def test_parity_200_steps_c3_tracking_drive():
+    """north_star on the headline config C3 (MuscleWalkingImitation2D-v0) with
+    live envs: 200 identical-action steps driven by a reference-tracking
+    excitation policy (tests/tracking.py: per-muscle stretch reflex toward
+    the reference row istep + 1, trunk balanced through the hips).  Half of
+    the 32 envs start from reset rows the drive keeps up for all 200 steps
+    in the oracle run, the other half from rows it falls from between steps
+    70 and 200, so the run covers long live trajectories and terminations.
+    Actions come from the oracle's state and go to both sides.
+
+    Under this drive the dynamics are not chaotic: the oracle against its
+    own one-ulp twin stays near 1e-10 for all 200 steps (computed here), so
+    the bound applies throughout: obs and reward within 1e-4 relative
+    (north_star) and within max(1e-7, 100 x the twin's error) on every env
+    alive on both sides at every step, `done` equal, and at least half the
+    envs alive at t = 200 on both the oracle and the GPU."""
+    import torch
+    from tracking import ROWS_FALL, ROWS_UP, TrackingDrive
+    from bioimitation.obslayout import load_names
+    env_id = 'MuscleWalkingImitation2D-v0'
+    rows = np.array(ROWS_UP + ROWS_FALL)
+    n, T = len(rows), 200
+    pk, env, orc, bufs = _setup(env_id, n, 64)
+    drive = TrackingDrive(orc, pk, load_names(env_id))
+    twin = orc.new_envs(n)
+    env.reset(ref_index=rows)
+    for i in range(n):
+        orc.reset(bufs, i, int(rows[i]))
+        orc.reset(twin, i, int(rows[i]))
+        s = orc.get_state(twin, i)
+        s[5] = np.nextafter(s[5], np.inf)        # one ulp in the first coordinate
+        orc.set_state(twin, i, s)
+    live = np.ones(n, bool)                      # alive on the GPU, the oracle and the twin
+    orc_alive, gpu_alive = np.ones(n, bool), np.ones(n, bool)
+    e_gpu, e_twin = np.zeros(T), np.zeros(T)
+    for t in range(T):
+        acts = np.stack([drive(orc.get_state(bufs, i)) for i in range(n)])
+        obs, rew, done = (v.cpu().numpy() for v in env.step(torch.as_tensor(acts, device=env.device))[:3])
+        for i in range(n):
+            o, r, d, _ = orc.step(bufs, i, acts[i])
+            o2, r2, d2, _ = orc.step(twin, i, acts[i])
+            if live[i]:
+                e_gpu[t] = max(e_gpu[t], _rel(obs[i], o).max(), abs(rew[i] - r) / max(1.0, abs(r)))
+                e_twin[t] = max(e_twin[t], _rel(o2, o).max(), abs(r2 - r) / max(1.0, abs(r)))
+                assert bool(done[i]) == d, (t, i)
+            orc_alive[i] &= not d
+            gpu_alive[i] &= not bool(done[i])
+            live[i] = live[i] and not (d or d2 or done[i])
+    ks = [0, 49, 99, 149, 199]
+    print(f'{env_id} 200 steps, tracking drive: alive at t=200 oracle {orc_alive.sum()}/{n}, GPU {gpu_alive.sum()}/{n}; '
+          f'max rel err GPU vs oracle / oracle vs its one-ulp twin at t=' +
+          ', '.join(f'{k + 1}: {e_gpu[k]:.1e} / {e_twin[k]:.1e}' for k in ks) + f'; overall {e_gpu.max():.1e}')
+    assert e_twin.max() <= 1e-5, e_twin.max()
+    assert e_gpu.max() < 1e-4, (int(e_gpu.argmax()), e_gpu.max())
+    assert (e_gpu <= np.maximum(1e-7, 100 * e_twin)).all(), int(np.argmax(e_gpu / np.maximum(1e-30, e_twin)))
+    assert orc_alive.sum() >= n // 2 and gpu_alive.sum() >= n // 2, (orc_alive.sum(), gpu_alive.sum())
     env.close()
