@@ -118,7 +118,7 @@ class ImitationEnv:
 
     # -- reference API -------------------------------------------------------
     def _out(self, obs, as_dict):
-        o = obs[0].double().cpu().numpy()
+        o = obs[0] if isinstance(obs, np.ndarray) else obs[0].double().cpu().numpy()
         if not as_dict:
             return o
         from .obslayout import load_names, obs_to_dict   # the reference's nested dict, rebuilt host-side

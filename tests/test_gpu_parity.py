@@ -548,32 +548,40 @@ def tracking_actions(pk, states, kp=1500.0, kd=80.0):
 def test_parity_200_steps_3d_envs_kept_up(env_id):
     """north_star's 200 identical-action steps on the spatial model with most
     envs alive to the end: a stiff reference-tracking PD (tracking_actions,
-    config horizon=1) keeps >= 50 % of 32 envs up for all 200 steps (the
-    oracle run of this drive: 21 / 24 of 32 with the perturbed twin below).
+    config horizon=1) keeps >= 50 % of 32 envs up for all 200 steps.
 
     Walking under a stiff PD held over 10 ms is chaotic: the oracle against
-    itself, started one ulp apart in one coordinate, drifts 4.5e-8 by t = 50,
-    1e-5 by t = 85 and O(1) by t = 150-200 (the twin curve, computed here).
-    No two fp64 implementations can then stay within 1e-4 over 200 steps;
-    what the HIP path must do is not diverge faster than that.  Bounds: obs
-    and reward within 1e-4 relative (north_star) and equal `done` for the
-    first 60 steps; afterwards, on envs alive on both sides, GPU-vs-oracle
-    error at most 100 x the twin's (or 1e-4); >= 50 % of the GPU's envs alive
-    at t = 200.  Actions come from the oracle's state and go to all sides."""
+    itself, started one ulp apart, drifts ~1e-8 by t = 50, ~1e-5 by t = 85 and
+    O(1) by t = 150-200.  No two fp64 implementations can then stay within
+    1e-4 over 200 steps; what the HIP path must do is not diverge faster than
+    the oracle does from its own rounding.  The reference for that is an
+    ensemble of four one-ulp twins (first coordinate, first speed, a joint
+    angle, a fiber-free joint speed), whose envelope (max over the twins)
+    stands for "a rounding-level perturbation" — the GPU's own first-step
+    difference (~1e-12) is one such perturbation in another direction, and a
+    single twin's curve swings by orders of magnitude against any other
+    direction's once the divergence is exponential.  Bounds: obs and reward
+    within 1e-4 relative (north_star) and equal `done` for the first 60 steps;
+    afterwards, on envs alive on all sides, GPU-vs-oracle error at most
+    100 x the twin envelope (or 1e-4); >= 50 % of the GPU's envs alive at
+    t = 200.  Actions come from the oracle's state and go to all sides."""
     import torch
     n, T, cfg = 32, 200, {'horizon': 1}
     pk, env, orc, bufs = _setup(env_id, n, 64, config=cfg)
-    twin = orc.new_envs(n)
+    nd = pk.ndof
+    perturb = [5, 5 + nd, 5 + nd // 2, 5 + nd + nd - 1]     # state columns nudged by one ulp
+    twins = [orc.new_envs(n) for _ in perturb]
     rng = np.random.default_rng(7)
     rows = rng.integers(0, min(pk.reset_hi, pk.n_episode - T) + 1, size=n)
     env.reset(ref_index=rows)
     for i in range(n):
         orc.reset(bufs, i, int(rows[i]))
-        orc.reset(twin, i, int(rows[i]))
-        s = orc.get_state(twin, i)
-        s[5] = np.nextafter(s[5], np.inf)        # one ulp in the first coordinate
-        orc.set_state(twin, i, s)
-    live = np.ones(n, bool)                      # alive on the oracle and the GPU
+        for tw, col in zip(twins, perturb):
+            orc.reset(tw, i, int(rows[i]))
+            s = orc.get_state(tw, i)
+            s[col] = np.nextafter(s[col], np.inf)
+            orc.set_state(tw, i, s)
+    live = np.ones(n, bool)                      # alive on the oracle, the twins and the GPU
     gpu_alive = np.ones(n, bool)
     e_gpu, e_twin = np.zeros(T), np.zeros(T)
     for t in range(T):
@@ -582,17 +590,21 @@ def test_parity_200_steps_3d_envs_kept_up(env_id):
         gpu_alive &= ~done.astype(bool)
         for i in np.where(live)[0]:
             o, r, d, _ = orc.step(bufs, i, acts[i])
-            o2, r2, d2, _ = orc.step(twin, i, acts[i])
             e = max(_rel(obs[i], o).max(), abs(rew[i] - r) / max(1.0, abs(r)))
             e_gpu[t] = max(e_gpu[t], e)
-            e_twin[t] = max(e_twin[t], _rel(o2, o).max(), abs(r2 - r) / max(1.0, abs(r)))
+            dt = False
+            for tw in twins:
+                o2, r2, d2, _ = orc.step(tw, i, acts[i])
+                e_twin[t] = max(e_twin[t], _rel(o2, o).max(), abs(r2 - r) / max(1.0, abs(r)))
+                dt = dt or d2
             if t < 60:
                 assert e < 1e-4, (t, i, e)
                 assert bool(done[i]) == d, (t, i)
-            live[i] = not (d or d2 or done[i])
+            live[i] = not (d or dt or done[i])
     ks = [0, 24, 49, 84, 99, 149, 199]
     print(f'{env_id} 200 steps, tracking drive: GPU alive at t=200 {gpu_alive.sum()}/{n}; max rel err GPU vs oracle / '
-          f'oracle vs its one-ulp twin at t=' + ', '.join(f'{k + 1}: {e_gpu[k]:.1e} / {e_twin[k]:.1e}' for k in ks))
+          f'oracle vs its one-ulp twins at t=' + ', '.join(f'{k + 1}: {e_gpu[k]:.1e} / {e_twin[k]:.1e}' for k in ks) +
+          f'; worst ratio after t=60 {np.max(e_gpu[60:] / np.maximum(1e-30, e_twin[60:])):.1f}')
     assert (e_gpu[60:] <= np.maximum(1e-4, 100 * e_twin[60:])).all(), np.argmax(e_gpu[60:] / np.maximum(1e-30, e_twin[60:]))
     assert gpu_alive.sum() >= n // 2
     env.close()
