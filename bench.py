@@ -220,6 +220,9 @@ def main():
             env.step(acts[k % pool])
     torch.cuda.synchronize(dev)
     resets0 = sum(h.reset_count() for h in handles)
+    rk = a.integrator == 'rk-merson'
+    rk = rk and all(hasattr(h._L, 'bioim_eval_count') for h in handles)   # older A/B builds lack the counter
+    evals0 = sum(h.eval_count() for h in handles) if rk else 0
 
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
@@ -287,6 +290,8 @@ def main():
             line['valu'] = valu
         if a.rk_budget:
             line['finished_env_steps'] = steps_total
+        if rk:
+            line['evals_per_env_step'] = (sum(h.eval_count() for h in handles) - evals0) / max(steps_local, 1)
         if not a.no_cpu_baseline and world == 1:
             line['cpu_baseline'] = cpu_baseline(a.env_id)
     env.close()
@@ -323,6 +328,8 @@ def reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist):
         fin += env.ready
         k0 += 1
     resets0 = env.reset_count()
+    counted = hasattr(env._L, 'bioim_eval_count')    # older A/B builds lack the counter
+    evals0 = env.eval_count() if counted else 0
     fin.zero_()
     if dist:
         dist.barrier()
@@ -347,6 +354,7 @@ def reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist):
     rate = {'value': tot / t_max, 'unit': 'finished env-steps/s', 'integrator': 'rk-merson', 'accuracy': 1e-3,
             'rk_budget': RK_BUDGET, 'launches': a.steps, 'ms_per_launch': t_max / a.steps * 1e3,
             'finished_env_steps': tot, 'done_rate': (env.reset_count() - resets0) / max(local, 1),
+            'evals_per_env_step': (env.eval_count() - evals0) / max(local, 1) if counted else None,
             'note': "the reference's integrator (opensim_wrapper.py:287-301) on the same workload; "
                     'GPU parity vs the oracle in tests/test_gpu_parity.py (RK) and tests/test_gpu_rk_budget.py'}
     env.close()

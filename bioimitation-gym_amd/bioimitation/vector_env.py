@@ -256,6 +256,13 @@ class VectorEnv:
         _lib.check(self._L.bioim_reset_count(self._h, C.byref(n)))
         return int(n.value)
 
+    def eval_count(self) -> int:
+        """Dynamics evaluations of the adaptive integrator so far over all envs
+        (bioim_eval_count)."""
+        n = C.c_uint64()
+        _lib.check(self._L.bioim_eval_count(self._h, C.byref(n)))
+        return int(n.value)
+
     def sync(self):
         _lib.check(self._L.bioim_sync(self._h))
 

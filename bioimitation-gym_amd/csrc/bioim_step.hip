@@ -2240,7 +2240,12 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     const bool budget = RK && a.rk_budget > 0;
     const bool resume = RK && mode == 0 && st.pend[env] != 0;
     bool suspend = false;
-    int launch_attempts = 0;
+    /* RK: dynamics evaluations spent in this launch (the budget is 5 per
+     * attempt); k1_ok: the first stage of the step from the current point is
+     * stored in st.rkf0 (a rejected attempt restarts from the same point, so
+     * its retry takes k1 from there and costs 4 evaluations instead of 5) */
+    int launch_evals = 0, evals = RK ? st.rkev[env] : 0;
+    bool k1_ok = false;
     int reset_row = 0;
     if (mode == 1) reset_row = a.ref_index ? a.ref_index[gidx] : draw_index(a.seed, a.env_offset + env, resets, M.reset_hi);
 
@@ -2313,6 +2318,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             if (NM > 0 && m < NM) D.ms[j].vN = st.vnw[(size_t)m * N + env];
         }
         rk_t = st.rkt[env]; rk_tf = t; rk_h = st.rkh[env]; rk_attempts = st.rka[env];
+        k1_ok = st.rkr[env] != 0;
         remaining = 1;
     } else if (mode == 0) {
         /* ---- action pre-processing (Env.step) */
@@ -2398,14 +2404,38 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     for (;;) {
         if constexpr (RK) {
             if (remaining > 0 && rk_stage == 0) {   /* start an RK step, or stop */
+                const int cost = k1_ok ? 4 : 5;
                 if (!(rk_tf - rk_t > 1e-14 * (1.0 + fabs(rk_tf)))) remaining = 0;
-                else if (budget && launch_attempts >= a.rk_budget) { suspend = true; break; }
+                else if (budget && launch_evals + cost > 5 * a.rk_budget) { suspend = true; break; }
                 else if (++rk_attempts > BIOIM_RK_MAX_ATTEMPTS) { rk_fail = true; remaining = 0; }
                 else {
-                    ++launch_attempts;
+                    launch_evals += cost;
                     rk_last = false;
                     if (rk_h >= rk_tf - rk_t) { rk_h = rk_tf - rk_t; rk_last = true; }
                     rk_err = 0;
+                    if (k1_ok) {
+                        /* retry of a rejected step: stage 0 from the stored k1 (same point,
+                         * time and controls), no dynamics call; the next call is stage 1 */
+                        const Real h = Real(rk_h);
+                        if (lane < ND) {
+                            const Real fq = ud, fu = st.rkf0[(size_t)lane * N + env];
+                            rk_update<Real>(0, h, fq, qd, y0q, Kq, Eq, rk_err);
+                            rk_update<Real>(0, h, fu, ud, y0u, Ku, Eu, rk_err);
+                        }
+                        if constexpr (NM > 0) {
+#pragma unroll
+                            for (int j = 0; j < MPL; ++j) {
+                                const int m = mslot<T>(lane + j * G);
+                                if (m < NM) {
+                                    const Real fa = st.rkf0[(size_t)(ND + m) * N + env];
+                                    const Real fl = st.rkf0[(size_t)(ND + NM + m) * N + env];
+                                    rk_update<Real>(0, h, fa, act[j], y0a[j], Ka[j], Ea[j], rk_err);
+                                    rk_update<Real>(0, h, fl, lce[j], y0l[j], Kl[j], El[j], rk_err);
+                                }
+                            }
+                        }
+                        rk_stage = 1;
+                    }
                 }
             }
         }
@@ -2450,10 +2480,13 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                                     RK ? Real(0) : (sub ? dt : Real(0)), eq && NM > 0, PA, pslot,
                                     RK ? 0 : M.nsub - remaining, D);
         }
+        if constexpr (RK) ++evals;
         if (RK && sub) {
             const Real h = Real(rk_h);
+            const bool s0 = rk_stage == 0;   /* k1 of this point: kept for a retry */
             if (lane < ND) {
                 const Real fq = ud, fu = D.qdd;
+                if (s0) st.rkf0[(size_t)lane * N + env] = fu;
                 rk_update<Real>(rk_stage, h, fq, qd, y0q, Kq, Eq, rk_err);
                 rk_update<Real>(rk_stage, h, fu, ud, y0u, Ku, Eu, rk_err);
             }
@@ -2463,6 +2496,10 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                     const int m = mslot<T>(lane + j * G);
                     if (m < NM) {
                         const Real fl = D.ms[j].clamped ? Real(0) : D.ms[j].vce;
+                        if (s0) {
+                            st.rkf0[(size_t)(ND + m) * N + env] = D.ms[j].dadt;
+                            st.rkf0[(size_t)(ND + NM + m) * N + env] = fl;
+                        }
                         rk_update<Real>(rk_stage, h, D.ms[j].dadt, act[j], y0a[j], Ka[j], Ea[j], rk_err);
                         rk_update<Real>(rk_stage, h, fl, lce[j], y0l[j], Kl[j], El[j], rk_err);
                     }
@@ -2489,10 +2526,12 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                 }
                 rk_t = rk_last ? rk_tf : rk_t + rk_h;
                 if (!rk_last) rk_hnext = rk_h * fac;
+                k1_ok = false;
             } else {
                 qd = y0q; ud = y0u;
 #pragma unroll
                 for (int j = 0; j < MPL; ++j) { act[j] = y0a[j]; lce[j] = y0l[j]; }
+                k1_ok = true;    /* same point: the retry reuses its stored k1 */
             }
             rk_h *= fac;
             continue;
@@ -2759,7 +2798,11 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         if (RK || mode == 1 || (osim && a.osim_op == BIOIM_OSIM_EQUILIBRATE)) st.hrk[env] = rk_hnext;
         if constexpr (RK) {
             st.pend[env] = suspend ? 1 : 0;
-            if (suspend) { st.rkt[env] = rk_t; st.rkh[env] = rk_h; st.rka[env] = rk_attempts; a.done_out[env] = 0; }
+            st.rkev[env] = evals;
+            if (suspend) {
+                st.rkt[env] = rk_t; st.rkh[env] = rk_h; st.rka[env] = rk_attempts; st.rkr[env] = k1_ok ? 1 : 0;
+                a.done_out[env] = 0;
+            }
             if (mode == 0 && a.ready_out) a.ready_out[env] = suspend ? 0 : 1;
         }
     }
@@ -3375,6 +3418,8 @@ template <typename Real> size_t state_layout(bioim_handle_t *h, char *base, DSta
     size_t opd = take(sizeof(int32_t) * n), ork = take(sizeof(double) * n), orh = take(sizeof(double) * n),
            ora = take(sizeof(int32_t) * n), octl = take(sizeof(Real) * na1 * n), ocur = take(sizeof(Real) * na1 * n),
            ovn = take(sizeof(Real) * nm1 * n);
+    size_t orr2 = take(sizeof(int32_t) * n), of0 = take(sizeof(Real) * (h->ndof + 2 * h->nmuscle) * n),
+           oev = take(sizeof(int32_t) * n);
     if (st) {
         st->q = (Real *)(base + oq); st->u = (Real *)(base + ou); st->act = (Real *)(base + oa);
         st->lce = (Real *)(base + ol); st->hist = (Real *)(base + oh); st->last = (Real *)(base + olast);
@@ -3384,6 +3429,7 @@ template <typename Real> size_t state_layout(bioim_handle_t *h, char *base, DSta
         st->pend = (int32_t *)(base + opd); st->rkt = (double *)(base + ork); st->rkh = (double *)(base + orh);
         st->rka = (int32_t *)(base + ora); st->ctl = (Real *)(base + octl); st->cur = (Real *)(base + ocur);
         st->vnw = (Real *)(base + ovn);
+        st->rkr = (int32_t *)(base + orr2); st->rkf0 = (Real *)(base + of0); st->rkev = (int32_t *)(base + oev);
     }
     return off;
 }
@@ -3800,6 +3846,28 @@ int bioim_reset_count(bioim_handle_t *h, uint64_t *total) {
         DState<float> hs;
         state_layout<float>(h, buf.data(), &hs);
         for (int e = 0; e < h->n; ++e) sum += (uint32_t)hs.resets[e];
+    }
+    *total = sum;
+    return 0;
+}
+
+/* dynamics evaluations of the RK integrator so far, summed over the envs */
+int bioim_eval_count(bioim_handle_t *h, uint64_t *total) {
+    if (!h || !total) return fail(BIOIM_E_ARG, "bioim_eval_count: bad arguments");
+    HIPCHK(hipSetDevice(h->device));
+    std::vector<char> buf(h->state_bytes);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipStreamSynchronize(h->side));
+    HIPCHK(hipMemcpy(buf.data(), h->state_buf, h->state_bytes, hipMemcpyDeviceToHost));
+    uint64_t sum = 0;
+    if (h->precision == 64) {
+        DState<double> hs;
+        state_layout<double>(h, buf.data(), &hs);
+        for (int e = 0; e < h->n; ++e) sum += (uint32_t)hs.rkev[e];
+    } else {
+        DState<float> hs;
+        state_layout<float>(h, buf.data(), &hs);
+        for (int e = 0; e < h->n; ++e) sum += (uint32_t)hs.rkev[e];
     }
     *total = sum;
     return 0;

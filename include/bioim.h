@@ -186,7 +186,9 @@ int bioim_set_state(bioim_handle_t *h, const double *host_state);
  * choice inside OsimModel.reset_manager. */
 int bioim_set_integrator(bioim_handle_t *h, int kind, double accuracy);
 /* Budgeted steps for the adaptive integrator (kind 1).  attempts > 0: each
- * bioim_step gives every env at most `attempts` Kutta-Merson step attempts;
+ * bioim_step gives every env at most 5 x `attempts` dynamics evaluations,
+ * i.e. `attempts` Kutta-Merson step attempts (a rejected attempt's retry
+ * costs 4, see bioim_eval_count);
  * an env whose env step is not finished by then is suspended at its last
  * accepted integration point and resumed by the next bioim_step (its action
  * row is ignored until it finishes).  ready_out (device [n], may be NULL)
@@ -200,6 +202,13 @@ int bioim_set_integrator(bioim_handle_t *h, int kind, double accuracy);
  * envs.  attempts = 0 restores one-step-per-launch.  No reference
  * counterpart (OpenSim steps one env at a time). */
 int bioim_set_rk_budget(bioim_handle_t *h, int attempts, uint8_t *ready_out);
+/* Dynamics evaluations the adaptive integrator (kind 1) has spent so far,
+ * summed over the handle's envs (an attempt costs 5; the retry of a rejected
+ * attempt 4: it restarts from the same point and reuses that point's first
+ * stage; the realize after each step 1).  Synchronizes the handle's streams.
+ * 0 for handles that never ran the adaptive integrator.  No reference
+ * counterpart (bench.py's evaluations per env step). */
+int bioim_eval_count(bioim_handle_t *h, uint64_t *total);
 /* envs suspended mid-step (synchronizes the handle's stream) */
 int bioim_pending_count(bioim_handle_t *h);
 /* Optional per-env step mask (device [n], NULL = every env steps): an env

@@ -113,8 +113,9 @@ class Oracle:
             raise ValueError('orc_env_set_integrator: bad arguments')
 
     def rk_stats(self, envs, i):
-        """(accepted steps, rejected steps, smallest step, next step) since set_integrator"""
-        out = np.zeros(4)
+        """(accepted steps, rejected steps, smallest step, next step, dynamics
+        evaluations) since set_integrator"""
+        out = np.zeros(5)
         self.lib.orc_env_rk_stats(self.env_ptr(envs, i), _ptr(out))
         return out
 

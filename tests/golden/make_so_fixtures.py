@@ -28,7 +28,9 @@ sys.path.insert(0, os.path.join(REPO, 'bioimitation-gym_amd'))
 from bioimitation.obslayout import load_names  # noqa: E402
 from bioimitation.storage import read_sto  # noqa: E402
 
-TRIALS = {'3D': ('3D', 'MuscleRunningImitation3D-v0')}
+TRIALS = {'3D': ('3D', 'MuscleRunningImitation3D-v0'),
+          # the palsy subject's model family: explicit Millard curve parameters (model_predictive.osim:1851-1870)
+          '02905': ('02905/02905_PRE', 'MusclePalsyImitation3D-v0')}
 
 
 def _vec(txt):
@@ -82,7 +84,15 @@ def main():
         rot = np.array(names['coord_rotational'], dtype=bool)
         if hdr.get('inDegrees', 'no').lower() == 'yes':
             q[:, rot] = np.deg2rad(q[:, rot])
-        grf_setup = re.sub(r'<!--.*?-->', '', open(os.path.join(d, 'experimental_data', 'setup_grf.xml')).read(), flags=re.S)
+        gpath = os.path.join(d, 'experimental_data', 'setup_grf.xml')
+        if not os.path.exists(gpath):
+            # 02905_PRE's setup_so.xml names ../experimental_data/setup_grf.xml, which the
+            # reference does not ship; its task_grf.mot has the 3D trial's columns
+            # (left_/right_ground_force_v*, _p*, left_/right_ground_torque_*), so the 3D
+            # trial's ExternalLoads mapping (same lab pipeline: right -> calcn_r, left -> calcn_l,
+            # force and point in ground) is used
+            gpath = os.path.join(DATA, '3D', 'experimental_data', 'setup_grf.xml')
+        grf_setup = re.sub(r'<!--.*?-->', '', open(gpath).read(), flags=re.S)
         ext = []
         for m in re.finditer(r'<ExternalForce name="([^"]+)">(.*?)</ExternalForce>', grf_setup, re.S):
             b = m.group(2)

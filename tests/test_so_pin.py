@@ -260,3 +260,32 @@ if __name__ == '__main__':
         so, tid, tso = balance(orc_mod, mut, **kw)
         r = ratios(so, tid, tso)
         print(f'{k:12s} ' + ' '.join(f'{c}={v:.4f}' for c, v in r.items()), f'({time.time() - t0:.1f}s)')
+
+
+def test_02905_static_optimization_is_not_reproducible_from_its_shipped_inputs(oracle_lib):
+    """The second shipped StaticOptimization run (data/02905/02905_PRE,
+    tests/golden/so_02905.npz) cannot pin the palsy model: its setup_so.xml
+    names ../experimental_data/setup_grf.xml, which the reference does not
+    ship, and no mapping of the shipped task_grf.mot onto the feet reproduces
+    the run.  Its residual actuators FX/FY/FZ/MX/MY/MZ absorb the whole-body
+    imbalance, so the pelvis translation rows must balance to ~1e-5 with the
+    loads the run actually had (the 3D trial: <= 1.2e-5, test above); with
+    the file's forces on calcn_l/calcn_r as labelled (the 3D trial's mapping)
+    or swapped, pelvis_ty misses by about its own RMS — e.g. at 1.10-1.25 s
+    the file has no vertical force while the run's FY stays under 20 N for a
+    343 N body weight.  Recorded as a finding; the joint-level pin stays the
+    3D trial's."""
+    z = dict(np.load(os.path.join(HERE, 'golden', 'so_02905.npz'), allow_pickle=False))
+    ty = []
+    for bodies in (z['grf_bodies'], z['grf_bodies'][::-1].copy()):
+        zz = dict(z, grf_bodies=bodies)
+        so = SOBalance(oracle_lib, zz)
+        ts = z['so_time'][::2]
+        tid, tso = (np.array(x) for x in zip(*(so.frame(t) for t in ts)))
+        ty.append(ratios(so, tid, tso)['pelvis_ty'])
+    assert min(ty) > 0.5, ty
+    names = list(z['so_names'])
+    fy = z['so_values'][:, names.index('FY')]
+    gy = z['grf'][:, :, 1].sum(1)
+    flight = np.interp(z['so_time'], z['grf_time'], gy) < 5.0
+    assert flight.sum() >= 10 and np.abs(fy[flight]).max() < 20.0
