@@ -102,6 +102,13 @@ def cpu_baseline(env_id, seconds=12.0):
         if eid != env_id:
             r, s = _cpu_rate(eid, cores, 3.0)
             extra[f'{tag}_{eid[:-3]}'] = {'value': r, 'unit': 'env-steps/s', 'cores': cores, 'sample': s}
+    # C5: the mixed LockedKnee3D + Palsy3D batch, half the threads on each ID
+    half = max(1, cores // 2)
+    rl, sl = _cpu_rate('MuscleLockedKneeImitation3D-v0', half, 3.0)
+    rp, sp = _cpu_rate('MusclePalsyImitation3D-v0', half, 3.0)
+    extra['C5_MuscleLockedKneeImitation3D+MusclePalsyImitation3D'] = {
+        'value': rl + rp, 'unit': 'env-steps/s', 'cores': 2 * half,
+        'sample': f'LockedKnee3D {sl} on {half} threads + Palsy3D {sp} on {half} threads, concurrently equivalent'}
     r, s = _cpu_rate(env_id, cores, 4.0, n_per_thread=16, integrator='rk-merson')
     extra[f'{env_id[:-3]}_rk_merson'] = {'value': r, 'unit': 'env-steps/s', 'cores': cores, 'sample': s,
                                          'integrator': 'RK-Merson 1e-3 (the reference integrator)'}
@@ -109,6 +116,34 @@ def cpu_baseline(env_id, seconds=12.0):
             'sample': f'{sample}, {env_id}, fp64 C oracle (CPU restatement, not OpenSim), {cores} threads = '
                       f'the CPUs this process may use (affinity, cgroup quota), auto-reset on host',
             'configs': extra}
+
+
+def single_env_rate(env_id, steps=300):
+    """The drop-in single-env path (bioimitation.envs.make(...).step, one env
+    per handle, one launch + host round trip per step; the reference's RLlib /
+    jaxrl scripts drive gym.make per worker this way), with and without the
+    save_simulation recorder (record_trajectory): env-steps/s next to C1."""
+    import numpy as np
+    from bioimitation import envs
+    out = {}
+    for rec in (True, False):
+        env = envs.make(env_id, config={'record_trajectory': rec})
+        rng = np.random.default_rng(0)
+        acts = rng.uniform(0.0, 1.0, size=(steps + 20, env.get_action_space_size()))
+        env.reset()
+        for k in range(20):
+            if env.step(acts[k])[2]:
+                env.reset()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            if env.step(acts[20 + k])[2]:
+                env.reset()
+        dt = time.perf_counter() - t0
+        env.close()
+        out['record_trajectory' if rec else 'no_recorder'] = {'value': steps / dt, 'unit': 'env-steps/s',
+                                                              'us_per_step': 1e6 * dt / steps}
+    out['note'] = f'{env_id}, 1 env on cuda:0, U[0,1] actions, {steps} timed steps (resets included)'
+    return out
 
 
 def _profile_record(name, key):
@@ -152,6 +187,7 @@ def main():
                     help='skip the second measurement: the same workload with the reference integrator '
                          '(RK-Merson 1e-3, budgeted launches), reported as "reference_integrator"')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-single-env', action='store_true', help='skip the single-env (envs.make) rate')
     ap.add_argument('--mixed', default=None,
                     help="mixed batch 'ID_A,ID_B' split 50/50 per GPU (BASELINE config C5), e.g. "
                          "MuscleLockedKneeImitation3D-v0,MusclePalsyImitation3D-v0")
@@ -294,6 +330,8 @@ def main():
             line['evals_per_env_step'] = (sum(h.eval_count() for h in handles) - evals0) / max(steps_local, 1)
         if not a.no_cpu_baseline and world == 1:
             line['cpu_baseline'] = cpu_baseline(a.env_id)
+        if world == 1 and not a.mixed and not a.no_single_env:
+            line['single_env'] = single_env_rate(a.env_id)
     env.close()
     if not (a.no_reference_integrator or a.mixed or a.integrator != 'semi-implicit'):
         ref = reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist)

@@ -113,6 +113,8 @@ class ImitationEnv:
         self._record = bool(cfg.get('record_trajectory', True))
         if self._record:
             self._env.enable_force_report()
+            if self._env.integrator == 'rk-merson':
+                self._env.enable_state_storage(512)    # the Manager's rows: every accepted step
         ntrans = sum(1 for c in (pk.coord_tx, pk.coord_ty, pk.coord_tz) if c >= 0)
         self._qdd = slice(1 + (pk.ncoord - ntrans) + pk.ncoord, 1 + (pk.ncoord - ntrans) + 2 * pk.ncoord)
 
@@ -126,10 +128,11 @@ class ImitationEnv:
             self._names = load_names(self.env_id)
         return obs_to_dict(o, self._env.pack, self._names)
 
-    def _record_row(self, obs):
+    def _record_row(self, obs, stepped=True):
         if self._record:
             fr = self._env.force_report[0].double().cpu().numpy()
-            self.osim_model.recorder.record(self._env.get_state()[0], obs[0, self._qdd].double().cpu().numpy(), fr)
+            self.osim_model.recorder.record(self._env.get_state()[0], obs[0, self._qdd].double().cpu().numpy(), fr,
+                                            storage=self.osim_model.storage() if stepped else None)
 
     def reset(self, obs_as_dict=False):
         index = 0 if self.test else random.randint(0, self._env.pack.reset_hi)
@@ -137,7 +140,7 @@ class ImitationEnv:
         self.osim_model._dirty()
         self.osim_model.recorder.clear()     # reset_manager re-initializes the analyses
         self._last = None
-        self._record_row(obs)
+        self._record_row(obs, stepped=False)
         return self._out(obs, obs_as_dict)
 
     def step(self, action, obs_as_dict=False):

@@ -12,8 +12,14 @@ trajectory since the last reset.
 
 Here the single-env API records the realized state after the reset and after
 every step, with the kernel's per-force-element report
-(``bioim_set_force_report``).  Differences from the reference:
-- One row per env step (0.01 s), not per internal RK-Merson step.
+(``bioim_set_force_report``).  With the reference's integrator
+(config ``integrator='rk-merson'``) the States storage holds, like the
+Manager's, the state after the reset and at every accepted Kutta-Merson step
+(``bioim_set_state_storage``).  Differences from the reference:
+- The Kinematics and ForceReporter analyses get one row per env step
+  (0.01 s); OpenSim's analyses record every integration step (step_interval
+  1), which would need a realize per accepted step.  With the fixed
+  semi-implicit substeps the States storage too has one row per env step.
 - ForceReporter columns: each muscle / coordinate actuator (its actuation),
   each Hunt-Crossley force's record values on the ground platform
   (``<force>.ground.force.X..Z``, ``.torque.X..Z``: the six values the
@@ -53,11 +59,23 @@ class TrajectoryRecorder:
     def clear(self):
         self.rows = []
         self.force_rows = []
+        self.state_rows = []
 
-    def record(self, state_row: np.ndarray, qdd: np.ndarray, forces: np.ndarray = None):
+    def _full(self, t, qd, ud, act, lce):
+        free = self.dof >= 0
+        q = self.default.copy()
+        u = np.zeros(self.nc)
+        q[free] = qd[self.dof[free]]
+        u[free] = ud[self.dof[free]]
+        return np.concatenate([[t], q, u, act, lce])
+
+    def record(self, state_row: np.ndarray, qdd: np.ndarray, forces: np.ndarray = None, storage=None):
         """state_row: one env's flat state (include/bioim.h layout);
         qdd: its observation's coordinate_acc block (all coordinates);
-        forces: its bioim_set_force_report row."""
+        forces: its bioim_set_force_report row; storage: the step's accepted
+        integration steps (bioim_set_state_storage rows: t, q, u, activation,
+        fiber length in dof order) — the States storage rows of the step
+        (default: the step's end state)."""
         if forces is not None:
             self.force_rows.append(np.concatenate([[float(state_row[0])], np.asarray(forces, dtype=np.float64)]))
         pk = self.pack
@@ -67,12 +85,15 @@ class TrajectoryRecorder:
         ud = state_row[5 + nd:5 + 2 * nd]
         act = state_row[5 + 2 * nd:5 + 2 * nd + nm]
         lce = state_row[5 + 2 * nd + nm:5 + 2 * nd + 2 * nm]
-        free = self.dof >= 0
-        q = self.default.copy()
-        u = np.zeros(self.nc)
-        q[free] = qd[self.dof[free]]
-        u[free] = ud[self.dof[free]]
-        self.rows.append(np.concatenate([[t], q, u, np.asarray(qdd, dtype=np.float64), act, lce]))
+        full = self._full(t, qd, ud, act, lce)
+        nc = self.nc
+        self.rows.append(np.concatenate([full[:1 + 2 * nc], np.asarray(qdd, dtype=np.float64), full[1 + 2 * nc:]]))
+        if storage is None:
+            self.state_rows.append(full)
+        else:
+            for r in np.asarray(storage, dtype=np.float64):
+                self.state_rows.append(self._full(r[0], r[1:1 + nd], r[1 + nd:1 + 2 * nd], r[1 + 2 * nd:1 + 2 * nd + nm],
+                                                  r[1 + 2 * nd + nm:1 + 2 * nd + 2 * nm]))
 
     # ------------------------------------------------------------------ output
     def _split(self):
@@ -86,18 +107,22 @@ class TrajectoryRecorder:
     def write(self, base_dir: str, prefix: str = 'simulation'):
         os.makedirs(base_dir, exist_ok=True)
         t, q, u, qdd, act, lce = self._split()
+        nc, nm = self.nc, self.pack.nmuscle
+        st = np.array(self.state_rows) if self.state_rows else np.zeros((0, 1 + 2 * nc + 2 * nm))
+        st_t, st_q, st_u = st[:, :1], st[:, 1:1 + nc], st[:, 1 + nc:1 + 2 * nc]
+        st_a, st_l = st[:, 1 + 2 * nc:1 + 2 * nc + nm], st[:, 1 + 2 * nc + nm:]
         coords = list(self.names['coords'])
         joints = list(self.names.get('coord_joints') or [''] * len(coords))
         rot = np.array(self.names.get('coord_rotational') or [True] * len(coords), dtype=bool)
         muscles = list(self.names['muscles']) if self.pack.nmuscle else []
         # Manager state storage (opensim_wrapper.py:336-337), interleaved per coordinate as OpenSim 4 orders them
-        labels, cols = ['time'], [t]
+        labels, cols = ['time'], [st_t]
         for i, (c, j) in enumerate(zip(coords, joints)):
             labels += [f'/jointset/{j}/{c}/value', f'/jointset/{j}/{c}/speed']
-            cols += [q[:, i:i + 1], u[:, i:i + 1]]
+            cols += [st_q[:, i:i + 1], st_u[:, i:i + 1]]
         for i, m in enumerate(muscles):
             labels += [f'/forceset/{m}/activation', f'/forceset/{m}/fiber_length']
-            cols += [act[:, i:i + 1], lce[:, i:i + 1]]
+            cols += [st_a[:, i:i + 1], st_l[:, i:i + 1]]
         paths = {}
         paths['states'] = os.path.join(base_dir, f'{prefix}_States.sto')
         write_sto(paths['states'], labels, np.hstack(cols), name='states')
@@ -293,7 +318,8 @@ class OsimModelFacade:
         fn(s[self._i])
         self._set_state(s)
         self._call('equilibrate')
-        self.recorder.clear()       # the new Manager's state storage starts here (:336)
+        self.recorder.clear()       # the new Manager's state storage starts here (:336) ...
+        self._record(stepped=False)  # ... with the initialized state (Manager.initialize)
 
     @property
     def istep(self):
@@ -362,9 +388,21 @@ class OsimModelFacade:
         self._call('integrate')
         self._record()
 
-    def _record(self):
+    def storage(self):
+        """the last env step's accepted integration steps (RK; None otherwise)"""
+        env = self._env
+        if getattr(env, 'storage_rows', None) is None:
+            return None
+        k = int(env.storage_count[self._i])
+        cap = env.storage_rows.shape[1]
+        if k > cap:
+            raise RuntimeError(f'state storage overflow: {k} accepted steps, capacity {cap}')
+        return env.storage_rows[self._i, :k].double().cpu().numpy()
+
+    def _record(self, stepped=True):
         r = self._rep
-        self.recorder.record(self._state()[self._i], r['qdd'], self._force_row(r))
+        self.recorder.record(self._state()[self._i], r['qdd'], self._force_row(r),
+                             storage=self.storage() if stepped else None)
 
     @staticmethod
     def _force_row(r):

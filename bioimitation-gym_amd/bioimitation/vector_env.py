@@ -148,6 +148,22 @@ class VectorEnv:
             self.force_report = None
         _lib.check(self._L.bioim_set_force_report(self._h, self._ptr(self.force_report)))
 
+    def enable_state_storage(self, capacity: int = 64):
+        """RK integrator: the state at every accepted integration step of each
+        env step in ``self.storage_rows`` (N, capacity, 1 + 2 ndof + 2 nm: t,
+        q, u, activation, fiber length) and their number in
+        ``self.storage_count`` (bioim_set_state_storage).  ``capacity=0`` turns
+        it off."""
+        import torch
+        if capacity:
+            d = 1 + 2 * self.pack.ndof + 2 * self.pack.nmuscle
+            self.storage_rows = torch.zeros((self.num_envs, capacity, d), dtype=self.dtype, device=self.device)
+            self.storage_count = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
+        else:
+            self.storage_rows = self.storage_count = None
+        _lib.check(self._L.bioim_set_state_storage(self._h, self._ptr(self.storage_rows), int(capacity),
+                                                   self._ptr(self.storage_count)))
+
     def set_rk_budget(self, attempts: int):
         """Budgeted steps for the 'rk-merson' integrator (``bioim_set_rk_budget``):
         each ``step()`` gives every env at most ``attempts`` Kutta-Merson step

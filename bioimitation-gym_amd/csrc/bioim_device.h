@@ -237,8 +237,5 @@ struct DState {
     int32_t *rka;   /* [N] attempts spent on the step so far                          */
     Real *ctl, *cur; /* [nact][N] its held controls and smoothed actions               */
     Real *vnw;      /* [nm][N] fiber-velocity warm starts (the last call's roots)      */
-    int32_t *rkr;   /* [N] 1: rkf0 holds k1 of the suspended step's current point      */
-    Real *rkf0;     /* [ndof + 2 nm][N] k1 (q'', da/dt, fiber velocity) of the last
-                     * attempt's start point: a rejected attempt's retry reuses it     */
     int32_t *rkev;  /* [N] dynamics evaluations so far (RK kernels; bioim_eval_count) */
 };

@@ -1944,6 +1944,12 @@ template <class T, typename Real> struct LaunchArgs {
     Real *final_obs;   /* optional: the step's observation before any auto-reset (row stride obs_stride) */
     Real *force_out;   /* optional: per-force-element values of the realized state, row stride force_dim */
     int force_dim;
+    /* optional (RK kernels): the Manager's state storage — a row (t, q, u,
+     * activation, fiber length) per accepted integration step of the env step,
+     * [N][traj_cap][traj_dim]; traj_n[N] counts them (past traj_cap: counted, not stored) */
+    Real *traj;
+    int32_t *traj_n;
+    int traj_cap, traj_dim;
     uint8_t *done_out;
     const int32_t *env_ids, *ref_index;
     uint64_t seed;
@@ -2241,11 +2247,14 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     const bool resume = RK && mode == 0 && st.pend[env] != 0;
     bool suspend = false;
     /* RK: dynamics evaluations spent in this launch (the budget is 5 per
-     * attempt); k1_ok: the first stage of the step from the current point is
-     * stored in st.rkf0 (a rejected attempt restarts from the same point, so
-     * its retry takes k1 from there and costs 4 evaluations instead of 5) */
+     * attempt) and so far (bioim_eval_count).  (Reusing a rejected attempt's
+     * first stage for its retry — same start point — saves about a fifth of
+     * the rejected attempts' evaluations but measured slower at 4096 envs:
+     * the stores of k1 cost every attempt, and the saving rarely removes a
+     * launch from a step; profiles/r03/ab_dropped/ab_rk_k1_reuse.txt) */
     int launch_evals = 0, evals = RK ? st.rkev[env] : 0;
-    bool k1_ok = false;
+    /* state-storage rows of this env step so far (a resumed step continues its count) */
+    int traj_k = (RK && a.traj && mode == 0 && st.pend[env] != 0) ? a.traj_n[env] : 0;
     int reset_row = 0;
     if (mode == 1) reset_row = a.ref_index ? a.ref_index[gidx] : draw_index(a.seed, a.env_offset + env, resets, M.reset_hi);
 
@@ -2318,7 +2327,6 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             if (NM > 0 && m < NM) D.ms[j].vN = st.vnw[(size_t)m * N + env];
         }
         rk_t = st.rkt[env]; rk_tf = t; rk_h = st.rkh[env]; rk_attempts = st.rka[env];
-        k1_ok = st.rkr[env] != 0;
         remaining = 1;
     } else if (mode == 0) {
         /* ---- action pre-processing (Env.step) */
@@ -2404,7 +2412,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     for (;;) {
         if constexpr (RK) {
             if (remaining > 0 && rk_stage == 0) {   /* start an RK step, or stop */
-                const int cost = k1_ok ? 4 : 5;
+                const int cost = 5;
                 if (!(rk_tf - rk_t > 1e-14 * (1.0 + fabs(rk_tf)))) remaining = 0;
                 else if (budget && launch_evals + cost > 5 * a.rk_budget) { suspend = true; break; }
                 else if (++rk_attempts > BIOIM_RK_MAX_ATTEMPTS) { rk_fail = true; remaining = 0; }
@@ -2413,29 +2421,6 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                     rk_last = false;
                     if (rk_h >= rk_tf - rk_t) { rk_h = rk_tf - rk_t; rk_last = true; }
                     rk_err = 0;
-                    if (k1_ok) {
-                        /* retry of a rejected step: stage 0 from the stored k1 (same point,
-                         * time and controls), no dynamics call; the next call is stage 1 */
-                        const Real h = Real(rk_h);
-                        if (lane < ND) {
-                            const Real fq = ud, fu = st.rkf0[(size_t)lane * N + env];
-                            rk_update<Real>(0, h, fq, qd, y0q, Kq, Eq, rk_err);
-                            rk_update<Real>(0, h, fu, ud, y0u, Ku, Eu, rk_err);
-                        }
-                        if constexpr (NM > 0) {
-#pragma unroll
-                            for (int j = 0; j < MPL; ++j) {
-                                const int m = mslot<T>(lane + j * G);
-                                if (m < NM) {
-                                    const Real fa = st.rkf0[(size_t)(ND + m) * N + env];
-                                    const Real fl = st.rkf0[(size_t)(ND + NM + m) * N + env];
-                                    rk_update<Real>(0, h, fa, act[j], y0a[j], Ka[j], Ea[j], rk_err);
-                                    rk_update<Real>(0, h, fl, lce[j], y0l[j], Kl[j], El[j], rk_err);
-                                }
-                            }
-                        }
-                        rk_stage = 1;
-                    }
                 }
             }
         }
@@ -2483,10 +2468,8 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         if constexpr (RK) ++evals;
         if (RK && sub) {
             const Real h = Real(rk_h);
-            const bool s0 = rk_stage == 0;   /* k1 of this point: kept for a retry */
             if (lane < ND) {
                 const Real fq = ud, fu = D.qdd;
-                if (s0) st.rkf0[(size_t)lane * N + env] = fu;
                 rk_update<Real>(rk_stage, h, fq, qd, y0q, Kq, Eq, rk_err);
                 rk_update<Real>(rk_stage, h, fu, ud, y0u, Ku, Eu, rk_err);
             }
@@ -2496,10 +2479,6 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                     const int m = mslot<T>(lane + j * G);
                     if (m < NM) {
                         const Real fl = D.ms[j].clamped ? Real(0) : D.ms[j].vce;
-                        if (s0) {
-                            st.rkf0[(size_t)(ND + m) * N + env] = D.ms[j].dadt;
-                            st.rkf0[(size_t)(ND + NM + m) * N + env] = fl;
-                        }
                         rk_update<Real>(rk_stage, h, D.ms[j].dadt, act[j], y0a[j], Ka[j], Ea[j], rk_err);
                         rk_update<Real>(rk_stage, h, fl, lce[j], y0l[j], Kl[j], El[j], rk_err);
                     }
@@ -2526,12 +2505,25 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                 }
                 rk_t = rk_last ? rk_tf : rk_t + rk_h;
                 if (!rk_last) rk_hnext = rk_h * fac;
-                k1_ok = false;
+                if (a.traj) {   /* the Manager stores every accepted step (opensim_wrapper.py:336) */
+                    if (traj_k < a.traj_cap) {
+                        Real *row = a.traj + ((size_t)env * a.traj_cap + traj_k) * a.traj_dim;
+                        if (lane == 0) row[0] = Real(rk_t);
+                        if (lane < ND) { row[1 + lane] = qd; row[1 + ND + lane] = ud; }
+                        if constexpr (NM > 0) {
+#pragma unroll
+                            for (int j = 0; j < MPL; ++j) {
+                                const int m = mslot<T>(lane + j * G);
+                                if (m < NM) { row[1 + 2 * ND + m] = act[j]; row[1 + 2 * ND + NM + m] = lce[j]; }
+                            }
+                        }
+                    }
+                    ++traj_k;
+                }
             } else {
                 qd = y0q; ud = y0u;
 #pragma unroll
                 for (int j = 0; j < MPL; ++j) { act[j] = y0a[j]; lce[j] = y0l[j]; }
-                k1_ok = true;    /* same point: the retry reuses its stored k1 */
             }
             rk_h *= fac;
             continue;
@@ -2799,8 +2791,9 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         if constexpr (RK) {
             st.pend[env] = suspend ? 1 : 0;
             st.rkev[env] = evals;
+            if (a.traj && (mode == 0 || (osim && a.osim_op == BIOIM_OSIM_INTEGRATE))) a.traj_n[env] = traj_k;
             if (suspend) {
-                st.rkt[env] = rk_t; st.rkh[env] = rk_h; st.rka[env] = rk_attempts; st.rkr[env] = k1_ok ? 1 : 0;
+                st.rkt[env] = rk_t; st.rkh[env] = rk_h; st.rka[env] = rk_attempts;
                 a.done_out[env] = 0;
             }
             if (mode == 0 && a.ready_out) a.ready_out[env] = suspend ? 0 : 1;
@@ -3261,6 +3254,9 @@ struct bioim_handle {
     int pert_n, pert_ob;
     void *final_obs;    /* caller's device buffer [n][obs_stride] or null (bioim_set_final_obs) */
     void *force_out;    /* caller's device buffer [n][force_dim] or null (bioim_set_force_report) */
+    void *traj;         /* caller's device buffers (bioim_set_state_storage) or null */
+    int32_t *traj_n;
+    int traj_cap;
     int rk;             /* integrator: 0 semi-implicit substeps (pack nsub), 1 RK-Merson (bioim_set_integrator) */
     double rk_acc;
     int rk_budget;      /* RK attempts per env per launch, 0: unbudgeted (bioim_set_rk_budget) */
@@ -3300,6 +3296,11 @@ LaunchArgs<T, Real> make_args(bioim_handle_t *h, int mode, const void *actions, 
     a.final_obs = mode == 0 ? reinterpret_cast<Real *>(h->final_obs) : nullptr;
     a.force_out = reinterpret_cast<Real *>(h->force_out);
     a.force_dim = h->nact + 6 * h->pack.ncforce + h->pack.nlimit;   /* bioim_force_report_dim */
+    const bool integrates = mode == 0 || (oc && oc->op == BIOIM_OSIM_INTEGRATE);
+    a.traj = integrates ? reinterpret_cast<Real *>(h->traj) : nullptr;
+    a.traj_n = h->traj_n;
+    a.traj_cap = h->traj_cap;
+    a.traj_dim = 1 + 2 * h->ndof + 2 * h->nmuscle;
     a.reward = reinterpret_cast<Real *>(reward);
     a.info = reinterpret_cast<Real *>(info);
     a.done_out = done;
@@ -3418,8 +3419,7 @@ template <typename Real> size_t state_layout(bioim_handle_t *h, char *base, DSta
     size_t opd = take(sizeof(int32_t) * n), ork = take(sizeof(double) * n), orh = take(sizeof(double) * n),
            ora = take(sizeof(int32_t) * n), octl = take(sizeof(Real) * na1 * n), ocur = take(sizeof(Real) * na1 * n),
            ovn = take(sizeof(Real) * nm1 * n);
-    size_t orr2 = take(sizeof(int32_t) * n), of0 = take(sizeof(Real) * (h->ndof + 2 * h->nmuscle) * n),
-           oev = take(sizeof(int32_t) * n);
+    size_t oev = take(sizeof(int32_t) * n);
     if (st) {
         st->q = (Real *)(base + oq); st->u = (Real *)(base + ou); st->act = (Real *)(base + oa);
         st->lce = (Real *)(base + ol); st->hist = (Real *)(base + oh); st->last = (Real *)(base + olast);
@@ -3429,7 +3429,7 @@ template <typename Real> size_t state_layout(bioim_handle_t *h, char *base, DSta
         st->pend = (int32_t *)(base + opd); st->rkt = (double *)(base + ork); st->rkh = (double *)(base + orh);
         st->rka = (int32_t *)(base + ora); st->ctl = (Real *)(base + octl); st->cur = (Real *)(base + ocur);
         st->vnw = (Real *)(base + ovn);
-        st->rkr = (int32_t *)(base + orr2); st->rkf0 = (Real *)(base + of0); st->rkev = (int32_t *)(base + oev);
+        st->rkev = (int32_t *)(base + oev);
     }
     return off;
 }
@@ -3680,6 +3680,14 @@ int bioim_pending_count(bioim_handle_t *h) {
 int bioim_force_report_dim(const bioim_handle_t *h) {
     if (!h) return fail(BIOIM_E_ARG, "null handle");
     return h->nact + 6 * h->pack.ncforce + h->pack.nlimit;
+}
+
+int bioim_set_state_storage(bioim_handle_t *h, void *rows, int capacity, int32_t *count) {
+    if (!h || (rows && (capacity <= 0 || !count))) return fail(BIOIM_E_ARG, "bioim_set_state_storage: bad arguments");
+    h->traj = rows;
+    h->traj_n = rows ? count : nullptr;
+    h->traj_cap = rows ? capacity : 0;
+    return 0;
 }
 
 int bioim_set_force_report(bioim_handle_t *h, void *force_out) {

@@ -186,9 +186,8 @@ int bioim_set_state(bioim_handle_t *h, const double *host_state);
  * choice inside OsimModel.reset_manager. */
 int bioim_set_integrator(bioim_handle_t *h, int kind, double accuracy);
 /* Budgeted steps for the adaptive integrator (kind 1).  attempts > 0: each
- * bioim_step gives every env at most 5 x `attempts` dynamics evaluations,
- * i.e. `attempts` Kutta-Merson step attempts (a rejected attempt's retry
- * costs 4, see bioim_eval_count);
+ * bioim_step gives every env at most `attempts` Kutta-Merson step attempts
+ * (5 dynamics evaluations each);
  * an env whose env step is not finished by then is suspended at its last
  * accepted integration point and resumed by the next bioim_step (its action
  * row is ignored until it finishes).  ready_out (device [n], may be NULL)
@@ -203,9 +202,8 @@ int bioim_set_integrator(bioim_handle_t *h, int kind, double accuracy);
  * counterpart (OpenSim steps one env at a time). */
 int bioim_set_rk_budget(bioim_handle_t *h, int attempts, uint8_t *ready_out);
 /* Dynamics evaluations the adaptive integrator (kind 1) has spent so far,
- * summed over the handle's envs (an attempt costs 5; the retry of a rejected
- * attempt 4: it restarts from the same point and reuses that point's first
- * stage; the realize after each step 1).  Synchronizes the handle's streams.
+ * summed over the handle's envs (5 per Kutta-Merson attempt, 1 per realize
+ * after a step or reset).  Synchronizes the handle's streams.
  * 0 for handles that never ran the adaptive integrator.  No reference
  * counterpart (bench.py's evaluations per env step). */
 int bioim_eval_count(bioim_handle_t *h, uint64_t *total);
@@ -231,6 +229,16 @@ int bioim_set_final_obs(bioim_handle_t *h, void *final_obs);
  * about the ground origin (3) on the feet] [per CoordinateLimitForce: its
  * generalized force].  NULL disables it. */
 int bioim_force_report_dim(const bioim_handle_t *h);
+/* Optional state storage of the adaptive integrator (kind 1): OpenSim's
+ * Manager stores the state at every accepted integration step, which
+ * save_simulation prints (opensim_wrapper.py:334-337).  When set, each env
+ * step (bioim_step, or bioim_osim INTEGRATE) writes per env one row per
+ * accepted Kutta-Merson step: rows [n][capacity][1 + 2 ndof + 2 nmuscle] =
+ * (time, q, u in dof order, activation, fiber length); count[n] receives the
+ * number of accepted steps of the env's last env step (rows beyond capacity
+ * are counted, not stored; a budgeted step's count spans its launches).
+ * Device buffers owned by the caller; rows = NULL disables it. */
+int bioim_set_state_storage(bioim_handle_t *h, void *rows, int capacity, int32_t *count);
 int bioim_set_force_report(bioim_handle_t *h, void *force_out);
 /* Sum over the handle's envs of their reset counters (explicit resets and
  * in-kernel auto-resets); synchronizes the handle's streams.  Lets a caller

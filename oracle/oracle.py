@@ -62,6 +62,8 @@ class Oracle:
             ('orc_osim_full_report_dim', C.c_int, [C.c_void_p]),
             ('orc_osim_full_report', None, [C.c_void_p, C.c_void_p, _dp]),
             ('orc_env_observe', None, [C.c_void_p, C.c_void_p, _dp]),
+            ('orc_env_set_state_storage', None, [C.c_void_p, _dp, C.c_int]),
+            ('orc_env_state_storage_count', C.c_int, [C.c_void_p]),
         ]:
             f = getattr(L, name)
             f.restype = res
@@ -154,6 +156,18 @@ class Oracle:
         out = np.zeros(self.lib.orc_osim_full_report_dim(self.pk))
         self.lib.orc_osim_full_report(self.pk, self.env_ptr(envs, i), _ptr(out))
         return out
+
+    def set_state_storage(self, envs, i, buf):
+        """buf: float64 array (capacity, 1 + 2 ndof + 2 nm) kept alive by the
+        caller, or None"""
+        if buf is None:
+            self.lib.orc_env_set_state_storage(self.env_ptr(envs, i), None, 0)
+        else:
+            assert buf.dtype == np.float64 and buf.flags.c_contiguous
+            self.lib.orc_env_set_state_storage(self.env_ptr(envs, i), _ptr(buf), buf.shape[0])
+
+    def state_storage_count(self, envs, i):
+        return self.lib.orc_env_state_storage_count(self.env_ptr(envs, i))
 
     def observe(self, envs, i):
         """env i's observation at its current state"""

@@ -172,7 +172,7 @@ def test_facade_actuate_integrate_matches_oracle(env_id, integrator):
             assert err[~acc].max() < 1e-4 and err[acc].max() < 1e-2, (t, err[~acc].max(), err[acc].max())
         assert om.istep == r
         assert split_osim_report(pk, got)['istep'] == r
-    assert len(om.recorder.rows) == 1 + 8     # the reset's row, then one per integrate
+    assert len(om.recorder.rows) == 1 + 8     # the env reset's row, then one per integrate
     env.close()
 
 
@@ -249,3 +249,52 @@ def test_env_public_methods():
     with pytest.raises(AttributeError):
         tenv.calc_cost_of_transport()
     tenv.close()
+
+
+def test_rk_state_storage_rows_match_oracle(tmp_path):
+    """save_simulation with the reference's integrator: simulation_States.sto
+    holds, like OpenSim's Manager storage (opensim_wrapper.py:334-337), the
+    reset state and the state at every accepted Kutta-Merson step
+    (bioim_set_state_storage); the rows equal the oracle's accepted steps of
+    the same episode (same count; values to 1e-9 relative — the step sizes
+    follow the error estimates, which agree to the rounding level)."""
+    import oracle
+    from bioimitation import envs
+    from bioimitation.storage import read_sto
+    env_id = 'MuscleWalkingImitation2D-v0'
+    env = envs.make(env_id, config={'integrator': 'rk-merson', 'mode': 'test'})
+    env.reset()
+    pk = env._env.pack
+    orc = oracle.Oracle(pk)
+    bufs = orc.new_envs(1)
+    orc.set_integrator(bufs, 0, 'rk-merson', 1e-3)
+    orc.reset(bufs, 0, 0)
+    d = 1 + 2 * pk.ndof + 2 * pk.nmuscle
+    store = np.zeros((512, d))
+    orc.set_state_storage(bufs, 0, store)
+    rng = np.random.default_rng(2)
+    want = [orc.get_state(bufs, 0)]
+    rows_orc = []
+    for t in range(6):
+        a = rng.uniform(0.0, 0.6, size=pk.nact)
+        env.step(a)
+        orc.step(bufs, 0, a)
+        k = orc.state_storage_count(bufs, 0)
+        rows_orc.append(store[:k].copy())
+    rows_orc = np.concatenate(rows_orc)
+    paths = env.osim_model.save_simulation(str(tmp_path))
+    h, labels, data = read_sto(paths['states'])
+    assert len(data) == 1 + len(rows_orc), (len(data), len(rows_orc))
+    np.testing.assert_allclose(data[1:, 0], rows_orc[:, 0], rtol=1e-9, atol=1e-12)
+    names = env.osim_model.coordinate_names
+    for c, n in enumerate(names):
+        dof = pk.coord[c].dof
+        if dof < 0:
+            continue
+        col = [i for i, l in enumerate(labels) if l.endswith(f'/{n}/value')][0]
+        np.testing.assert_allclose(data[1:, col], rows_orc[:, 1 + dof], rtol=1e-9, atol=1e-9)
+    m0 = env.osim_model.muscle_names[0]
+    col = labels.index(f'/forceset/{m0}/fiber_length')
+    np.testing.assert_allclose(data[1:, col], rows_orc[:, 1 + 2 * pk.ndof + pk.nmuscle], rtol=1e-9, atol=1e-9)
+    assert len(rows_orc) > 6 * 3        # several accepted steps per 0.01 s env step
+    env.close()
