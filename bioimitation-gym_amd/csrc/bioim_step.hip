@@ -2233,10 +2233,8 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
 #pragma unroll
             for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
                 hist[j][hh] = hh < H ? st.hist[((size_t)hh * NA + m) * N + env] : Real(0);
-            /* held controls: the PrescribedController's Constant functions keep
-             * the last actuate() through OsimModel.reset (opensim_wrapper.py:92-107,
-             * :293-297), so a reset realizes with them */
-            if (mode != 0) control[j] = st.ctl[(size_t)m * N + env];
+            /* held controls (OsimModel calls act on the last actuate) */
+            if (osim) control[j] = st.ctl[(size_t)m * N + env];
         }
     }
     int done = 0;
@@ -2252,7 +2250,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
      * the rejected attempts' evaluations but measured slower at 4096 envs:
      * the stores of k1 cost every attempt, and the saving rarely removes a
      * launch from a step; profiles/r03/ab_dropped/ab_rk_k1_reuse.txt) */
-    int launch_evals = 0, evals = RK ? st.rkev[env] : 0;
+    int launch_evals = 0;
     /* state-storage rows of this env step so far (a resumed step continues its count) */
     int traj_k = (RK && a.traj && mode == 0 && st.pend[env] != 0) ? a.traj_n[env] : 0;
     int reset_row = 0;
@@ -2311,6 +2309,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                 const Real hi = NM > 0 ? Real(1) : SM.ca_max[ms];
                 const Real v = anynan ? Real(0) : raw[j];
                 control[j] = m < NA ? (v < lo ? lo : (v > hi ? hi : v)) : Real(0);
+                if (m < NA) st.ctl[(size_t)m * N + env] = control[j];
             }
         }
         if (a.osim_op == BIOIM_OSIM_INTEGRATE) begin_integrate();
@@ -2400,6 +2399,10 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             const Real hi = NM > 0 ? Real(1) : SM.ca_max[ms];
             const Real v = pnan ? Real(0) : control[j];
             control[j] = m < NA ? (v < lo ? lo : (v > hi ? hi : v)) : Real(0);
+            /* the held controls (PrescribedController's Constants): kept through
+             * resets, read by resets and OsimModel calls; stored now, so they
+             * are not held in registers past the last dynamics call */
+            if (m < NA) st.ctl[(size_t)m * N + env] = control[j];
         }
         /* ---- integrate to step_size * istep */
         begin_integrate();
@@ -2437,13 +2440,18 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             istep = M.ref_istep[r];
             has_last = 0;
             rk_hnext = 0;   /* reset_manager: a new integrator (opensim_wrapper.py:287-291) */
-            /* initializeState: the default activation (the held controls stay) */
-            if constexpr (NM > 0) {
+            /* initializeState: the default activation.  The held controls stay:
+             * the PrescribedController's Constant functions keep the last
+             * actuate() through OsimModel.reset (opensim_wrapper.py:92-107,
+             * :293-297), so a reset realizes with them — reloaded from HBM
+             * (stored when the step computed them) rather than kept in
+             * registers through the report (+40 VGPRs in 3D fp64) */
 #pragma unroll
-                for (int j = 0; j < MPL; ++j) {
-                    const int m = mslot<T>(lane + j * G);
+            for (int j = 0; j < MPL; ++j) {
+                const int m = mslot<T>(lane + j * G);
+                control[j] = m < NA ? st.ctl[(size_t)m * N + env] : Real(0);
+                if constexpr (NM > 0)
                     if (m < NM) act[j] = SM.mus[m].default_act;
-                }
             }
             resets += 1;
         }
@@ -2465,7 +2473,6 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                                     RK ? Real(0) : (sub ? dt : Real(0)), eq && NM > 0, PA, pslot,
                                     RK ? 0 : M.nsub - remaining, D);
         }
-        if constexpr (RK) ++evals;
         if (RK && sub) {
             const Real h = Real(rk_h);
             if (lane < ND) {
@@ -2790,22 +2797,14 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         if (RK || mode == 1 || (osim && a.osim_op == BIOIM_OSIM_EQUILIBRATE)) st.hrk[env] = rk_hnext;
         if constexpr (RK) {
             st.pend[env] = suspend ? 1 : 0;
-            st.rkev[env] = evals;
+            /* evaluations: the attempts', plus one realize per finished step and per reset */
+            st.rkev[env] += launch_evals + (suspend ? 0 : 1) + (do_reset && mode == 0 ? 1 : 0);
             if (a.traj && (mode == 0 || (osim && a.osim_op == BIOIM_OSIM_INTEGRATE))) a.traj_n[env] = traj_k;
             if (suspend) {
                 st.rkt[env] = rk_t; st.rkh[env] = rk_h; st.rka[env] = rk_attempts;
                 a.done_out[env] = 0;
             }
             if (mode == 0 && a.ready_out) a.ready_out[env] = suspend ? 0 : 1;
-        }
-    }
-    /* the held controls (a step's actuate, or an OsimModel.actuate): kept
-     * through resets, read by resets and OsimModel calls */
-    if (mode == 0 || (osim && a.controls_in)) {
-#pragma unroll
-        for (int j = 0; j < MPL; ++j) {
-            const int m = mslot<T>(lane + j * G);
-            if (m < NA) st.ctl[(size_t)m * N + env] = control[j];
         }
     }
     if (RK && suspend) {

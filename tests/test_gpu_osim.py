@@ -285,16 +285,16 @@ def test_rk_state_storage_rows_match_oracle(tmp_path):
     paths = env.osim_model.save_simulation(str(tmp_path))
     h, labels, data = read_sto(paths['states'])
     assert len(data) == 1 + len(rows_orc), (len(data), len(rows_orc))
-    np.testing.assert_allclose(data[1:, 0], rows_orc[:, 0], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(data[1:, 0], rows_orc[:, 0], rtol=0, atol=1e-9)   # step sizes: rounding-level
     names = env.osim_model.coordinate_names
     for c, n in enumerate(names):
         dof = pk.coord[c].dof
         if dof < 0:
             continue
         col = [i for i, l in enumerate(labels) if l.endswith(f'/{n}/value')][0]
-        np.testing.assert_allclose(data[1:, col], rows_orc[:, 1 + dof], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(data[1:, col], rows_orc[:, 1 + dof], rtol=1e-6, atol=1e-8)
     m0 = env.osim_model.muscle_names[0]
     col = labels.index(f'/forceset/{m0}/fiber_length')
-    np.testing.assert_allclose(data[1:, col], rows_orc[:, 1 + 2 * pk.ndof + pk.nmuscle], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(data[1:, col], rows_orc[:, 1 + 2 * pk.ndof + pk.nmuscle], rtol=1e-6, atol=1e-8)
     assert len(rows_orc) > 6 * 3        # several accepted steps per 0.01 s env step
     env.close()

@@ -1,13 +1,20 @@
 #!/bin/bash
 # Per-kernel register / scratch / LDS usage of libbioim's kernels (gfx950),
-# from the compiler's kernel-resource-usage remarks.  CPU only.
+# from the compiler's kernel-resource-usage remarks, one topology per job
+# (the shipped per-topology units, in parallel).  CPU only.
 #   bash tools/resources.sh [extra hipcc flags]
 set -e
 cd "$(dirname "$0")/.."
 # the shipped library's flags (bioimitation/_buildinfo.py: one place for them)
 FLAGS=$(cd bioimitation-gym_amd && python3 -m bioimitation._buildinfo flags)
-hipcc $FLAGS -c --offload-device-only \
-    -Rpass-analysis=kernel-resource-usage "$@" -o /tmp/bioim_res.o bioimitation-gym_amd/csrc/bioim_step.hip 2>&1 |
+NT=$(sed -n 's/#define BIOIM_NTOPOLOGIES \([0-9]*\)/\1/p' bioimitation-gym_amd/csrc/topologies.h)
+tmp=$(mktemp -d)
+for k in $(seq 0 $((NT - 1))); do
+  hipcc $FLAGS -DBIOIM_TOPO_ONLY=$k -c --offload-device-only \
+      -Rpass-analysis=kernel-resource-usage "$@" -o $tmp/res$k.o bioimitation-gym_amd/csrc/bioim_step.hip > $tmp/res$k.txt 2>&1 &
+done
+wait
+cat $tmp/res*.txt |
     python3 -c "
 import re, sys
 cur = None
@@ -20,6 +27,8 @@ for l in sys.stdin:
     if m and cur is not None:
         cur[m.group(1).split(' ')[0]] = int(m.group(2))
 for r in rows:
-    n = re.sub(r'^_Z\d+', '', r['name'])[:60]
-    print(f\"{n:60s} VGPR {r.get('VGPRs','?'):>4} AGPR {r.get('AGPRs','?'):>4} SGPR {r.get('SGPRs','?'):>4} scratch {r.get('ScratchSize','?'):>5}\")
+    n = re.sub(r'^_Z\d+', '', r['name'])[:64]
+    v, a = r.get('VGPRs', 0), r.get('AGPRs', 0)
+    print(f\"{n:64s} VGPR {v:>4} AGPR {a:>4} total {v + a:>4} SGPR {r.get('SGPRs','?'):>4} scratch {r.get('ScratchSize','?'):>5}\")
 "
+rm -rf $tmp
