@@ -118,18 +118,25 @@ def cpu_baseline(env_id, seconds=12.0):
             'configs': extra}
 
 
-def single_env_rate(env_id, steps=300):
+def single_env_rate(env_id='TorqueWalkingImitation2D-v0', steps=300):
     """The drop-in single-env path (bioimitation.envs.make(...).step, one env
     per handle, one launch + host round trip per step; the reference's RLlib /
     jaxrl scripts drive gym.make per worker this way), with and without the
-    save_simulation recorder (record_trajectory): env-steps/s next to C1."""
+    save_simulation recorder (record_trajectory): env-steps/s on C1's config
+    (TorqueWalkingImitation2D-v0, 1 env), next to C1's CPU time per step."""
     import numpy as np
     from bioimitation import envs
+    from bioimitation.registry import load_pack
+    pk = load_pack(env_id)
     out = {}
     for rec in (True, False):
         env = envs.make(env_id, config={'record_trajectory': rec})
         rng = np.random.default_rng(0)
-        acts = rng.uniform(0.0, 1.0, size=(steps + 20, env.get_action_space_size()))
+        if pk.nmuscle:
+            acts = rng.uniform(0.0, 1.0, size=(steps + 20, pk.nact))
+        else:   # PD targets near the reference (SURVEY.md 8d)
+            base = np.array([pk.ref_q[60][pk.pd_coord[a]] for a in range(pk.nact)])
+            acts = base + rng.normal(0.0, 0.05, size=(steps + 20, pk.nact))
         env.reset()
         for k in range(20):
             if env.step(acts[k])[2]:
@@ -142,7 +149,9 @@ def single_env_rate(env_id, steps=300):
         env.close()
         out['record_trajectory' if rec else 'no_recorder'] = {'value': steps / dt, 'unit': 'env-steps/s',
                                                               'us_per_step': 1e6 * dt / steps}
-    out['note'] = f'{env_id}, 1 env on cuda:0, U[0,1] actions, {steps} timed steps (resets included)'
+    out['note'] = (f'{env_id}, 1 env on cuda:0, {steps} timed steps (resets included); a step is a full '
+                   f'kernel (nsub substeps) plus a host round trip: latency-bound by design (the batched '
+                   f'VectorEnv is the throughput path)')
     return out
 
 
@@ -331,7 +340,7 @@ def main():
         if not a.no_cpu_baseline and world == 1:
             line['cpu_baseline'] = cpu_baseline(a.env_id)
         if world == 1 and not a.mixed and not a.no_single_env:
-            line['single_env'] = single_env_rate(a.env_id)
+            line['single_env'] = single_env_rate()
     env.close()
     if not (a.no_reference_integrator or a.mixed or a.integrator != 'semi-implicit'):
         ref = reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist)

@@ -128,10 +128,11 @@ class ImitationEnv:
             self._names = load_names(self.env_id)
         return obs_to_dict(o, self._env.pack, self._names)
 
-    def _record_row(self, obs, stepped=True):
+    def _record_row(self, o, stepped=True):
+        """o: the env's observation row on the host"""
         if self._record:
             fr = self._env.force_report[0].double().cpu().numpy()
-            self.osim_model.recorder.record(self._env.get_state()[0], obs[0, self._qdd].double().cpu().numpy(), fr,
+            self.osim_model.recorder.record(self._env.get_state()[0], o[self._qdd], fr,
                                             storage=self.osim_model.storage() if stepped else None)
 
     def reset(self, obs_as_dict=False):
@@ -140,8 +141,9 @@ class ImitationEnv:
         self.osim_model._dirty()
         self.osim_model.recorder.clear()     # reset_manager re-initializes the analyses
         self._last = None
-        self._record_row(obs, stepped=False)
-        return self._out(obs, obs_as_dict)
+        o = obs[0].double().cpu().numpy()
+        self._record_row(o, stepped=False)
+        return self._out(o[None, :], obs_as_dict)
 
     def step(self, action, obs_as_dict=False):
         import torch
@@ -149,10 +151,14 @@ class ImitationEnv:
                             device=self._env.device)
         obs, rew, done, info = self._env.step(a)
         self.osim_model._dirty()
-        self._record_row(obs)
-        info = [float(v) for v in info[0].double().cpu().numpy()]
-        self._last = (float(rew[0]), info, bool(done[0]))
-        return [self._out(obs, obs_as_dict), self._last[0], self._last[2], {'all_rewards': info}]
+        # one device-to-host copy for the step's outputs (each .cpu() waits on the stream)
+        out = torch.cat([obs[0], rew[:1], info[0], done[:1].to(obs.dtype)]).double().cpu().numpy()
+        nobs, ninf = obs.shape[1], info.shape[1]
+        o = out[:nobs]
+        self._record_row(o)
+        inf = [float(v) for v in out[nobs + 1:nobs + 1 + ninf]]
+        self._last = (float(out[nobs]), inf, bool(out[-1]))
+        return [self._out(o[None, :], obs_as_dict), self._last[0], self._last[2], {'all_rewards': inf}]
 
     # -- the task envs' public methods (muscle_walking_imitation_env2D.py:102-403,
     #    opensim_environment.py:52-98); realizations run on the GPU (bioim_osim) --
