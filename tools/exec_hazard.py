@@ -12,7 +12,19 @@ the region (the value is live in every lane) and its destination is read
 after the join before being rewritten, the inactive lanes read whatever the
 destination held before: a value silently lost in those lanes.  The scan is
 linear over each kernel (loop back-edges are ignored), so it reports
-candidates; each must be checked by hand.
+candidates, each classified:
+
+  phi-merge   the destination's last write before the region was made with
+              EXEC at least as wide as the region's parent (a well-defined
+              value in the lanes the region leaves out): the copy is the
+              ISA form of `x = cond ? new : x_old` — what the source code asks
+              for, not an allocator split; benign;
+  masked-use  no such earlier write, but every read after the join until
+              the next full write happens inside a narrowed region again
+              (the lanes that skipped the copy may be masked off there too:
+              check that the two conditions select the same lanes);
+  undefined   no earlier write and a read under wider EXEC: lanes outside
+              the region read a register nothing wrote — the hazard.
 
     python tools/exec_hazard.py <file.s> [kernel-substring]
 """
@@ -50,19 +62,57 @@ def parse(lines):
     return ins
 
 
+def is_join(op, raw):
+    return op == 's_or_b64' and raw.split(None, 1)[1].startswith('exec, exec,')
+
+
+def depths(ins):
+    """EXEC nesting depth at each instruction (0: the kernel's full EXEC)"""
+    out, stack = [], []
+    for op, dst, src, raw in ins:
+        if op in ('s_and_saveexec_b64', 's_or_saveexec_b64', 's_andn2_saveexec_b64'):
+            out.append(len(stack))
+            stack.append(raw.split(None, 1)[1].split(',')[0].strip())
+            continue
+        if op == 's_mov_b64' and raw.split(None, 1)[1].endswith(', exec'):
+            # EXEC saved by a plain move (a loop or an if/else whose then-part
+            # re-narrows with s_mov_b64 exec, ...): restored by s_or_b64 with it
+            out.append(len(stack))
+            stack.append(raw.split(None, 1)[1].split(',')[0].strip())
+            continue
+        if is_join(op, raw):
+            sv = raw.split(',')[-1].strip()
+            if sv in stack:        # a restore of a mask this scan did not see saved is not a join
+                while stack.pop() != sv:
+                    pass
+        out.append(len(stack))
+    return out
+
+
+def classify(ins, dep, i, start, dst, join_read):
+    """phi-merge / masked-use / undefined for the candidate copy at i in the
+    region opened at `start` (module docstring)"""
+    parent = dep[start]
+    for j in range(start - 1, -1, -1):
+        if any(d in ins[j][1] for d in dst):
+            return 'phi-merge' if dep[j] <= parent else 'masked-use'
+    return 'masked-use' if dep[join_read] > 0 else 'undefined'
+
+
 def scan(ins):
     hits = []
+    dep = depths(ins)
     stack = []   # open regions: (saved-exec sgpr text, start index)
     for i, (op, dst, src, raw) in enumerate(ins):
-        if op in ('s_and_saveexec_b64', 's_or_saveexec_b64', 's_andn2_saveexec_b64'):
+        if op in ('s_and_saveexec_b64', 's_or_saveexec_b64', 's_andn2_saveexec_b64') or \
+                (op == 's_mov_b64' and raw.split(None, 1)[1].endswith(', exec')):
             stack.append((raw.split(None, 1)[1].split(',')[0].strip(), i))
             continue
-        if op == 's_or_b64' and raw.split(None, 1)[1].startswith('exec, exec,'):
+        if is_join(op, raw):
             sv = raw.split(',')[-1].strip()
-            while stack:
-                s, _ = stack.pop()
-                if s == sv:
-                    break
+            if any(s == sv for s, _ in stack):
+                while stack.pop()[0] != sv:
+                    pass
             continue
         if not stack or op not in ('v_accvgpr_write_b32', 'v_accvgpr_read_b32', 'v_mov_b32', 'v_mov_b64'):
             continue
@@ -85,7 +135,7 @@ def scan(ins):
         verdict = None
         while j < len(ins) and verdict is None:
             o, dd, ss, rr = ins[j]
-            if o == 's_or_b64' and rr.split(None, 1)[1].startswith('exec, exec,') and rr.split(',')[-1].strip() == inner_sv:
+            if is_join(o, rr) and rr.split(',')[-1].strip() == inner_sv:
                 closed = True
             if any(x in ss for x in dst):
                 verdict = 'read-after-join' if closed else 'read-inside'
@@ -93,7 +143,7 @@ def scan(ins):
                 verdict = 'overwritten'
             j += 1
         if verdict == 'read-after-join':
-            hits.append((i, raw, j - 1, ins[j - 1][3]))
+            hits.append((i, raw, j - 1, ins[j - 1][3], classify(ins, dep, i, start, dst, j - 1)))
     return hits
 
 
@@ -109,9 +159,10 @@ def main():
         e = next(i for i in range(s, len(text)) if text[i].startswith('.Lfunc_end'))
         ins = parse(text[s:e])
         hits = scan(ins)
-        print(f'{name[:90]}: {len(ins)} instructions, {len(hits)} candidate copies')
-        for i, raw, j, use in hits[:12]:
-            print(f'    [{i}] {raw:50s} -> read after join at [{j}] {use}')
+        kinds = {k: sum(1 for h in hits if h[4] == k) for k in ('phi-merge', 'masked-use', 'undefined')}
+        print(f'{name[:90]}: {len(ins)} instructions, {len(hits)} candidate copies {kinds}')
+        for i, raw, j, use, kind in hits:
+            print(f'    [{i}] {raw:50s} -> read after join at [{j}] {use:45s} {kind}')
 
 
 if __name__ == '__main__':
