@@ -504,7 +504,7 @@ template <class T, typename Real> struct Lay {
     static constexpr int MF = LIM + 4 * NL;      /* [NSLOT][3]: function slots f, f', f''           */
     static constexpr int U = ((MF + 3 * (NSLOT > 0 ? NSLOT : 1) + 1) / 2) * 2;
     static constexpr int LOC = U;                /* phase 1: [NB+1][24] joint-local data (NB: identity) */
-    static constexpr int SL = LOC + 24 * (NB + 1); /* phase 1: [ND][6] joint-local Plucker columns  */
+    static constexpr int SL = LOC + 24 * (NB + 1); /* phase 1: [ND][6] joint-local Plucker columns, + sink row */
     /* phases 2-3: [MPL * G][MAXSPAN] per muscle slot, -F_t dL/dq over its
      * span (actuator slot: its torque), then one zero slot (TZ) */
     static constexpr int TZ = MPL * T::G * T::MAXSPAN;
@@ -513,7 +513,7 @@ template <class T, typename Real> struct Lay {
     static constexpr int CJ = TAU + TAUN;        /* phases 2-3: [NS][CJN] contact slots             */
     static constexpr int OBS = U;                /* report: observation staging                     */
     static constexpr int REP = OBS + OBSMAX;     /* report: [NOS+1][6] body pos/vel (NOS: COM)      */
-    static constexpr int U1 = 24 * (NB + 1) + 6 * ND, U2 = TAUN + NS * CJN;
+    static constexpr int U1 = 24 * (NB + 1) + 6 * (ND + 1), U2 = TAUN + NS * CJN;
     static constexpr int U3 = OBSMAX + 6 * (T::NOS + 1);
     static constexpr int USZ = U1 > U2 ? (U1 > U3 ? U1 : U3) : (U2 > U3 ? U2 : U3);
     static constexpr int SIZE = ((U + USZ + 1) / 2) * 2;
@@ -630,8 +630,17 @@ DEV void kin_local(const SModel<T, Real> &SM, Real *lds, int c) {
                 if (kind == BIOIM_FN_CONST) f = fb;
             }
             if constexpr ((KM & (1u << (BIOIM_FN_SPLINE + 1))) != 0) {
-                if (kind == BIOIM_FN_SPLINE) {   /* spline axes: evaluated in phase 0b */
-                    const int jj = js >= 0 ? js : 0;
+                /* spline axes: evaluated in phase 0b.  Planar: loaded
+                 * unconditionally (slot 0 for the other kinds) and selected,
+                 * no branch (same-box Torque2D -3 %, 2D -0.7 % with the
+                 * branch-free SL and subtree sums; no gain in 3D, where it
+                 * costs registers: profiles/r03/ab_subtree.txt) */
+                const int jj = js >= 0 ? js : 0;
+                if constexpr (T::PLANAR) {
+                    const bool sp = kind == BIOIM_FN_SPLINE;
+                    const Real sf = lds[LY::MF + 3 * jj], sf1 = lds[LY::MF + 3 * jj + 1], sf2 = lds[LY::MF + 3 * jj + 2];
+                    f = sp ? sf : f; f1 = sp ? sf1 : f1; f2 = sp ? sf2 : f2;
+                } else if (kind == BIOIM_FN_SPLINE) {
                     f = lds[LY::MF + 3 * jj]; f1 = lds[LY::MF + 3 * jj + 1]; f2 = lds[LY::MF + 3 * jj + 2];
                 }
             }
@@ -715,8 +724,10 @@ DEV void kin_local(const SModel<T, Real> &SM, Real *lds, int c) {
     sfor<0, 6>([&](auto aI) {
         constexpr int ax = decltype(aI)::value;
         if constexpr (((USED >> ax) & 1u) != 0) {
-            if (cd[ax] >= 0) {
-                Real *sl = lds + LY::SL + 6 * cd[ax];
+            /* planar: an axis without a dof accumulates into the sink row
+             * SL[ND] (no branch) */
+            if (T::PLANAR || cd[ax] >= 0) {
+                Real *sl = lds + LY::SL + 6 * (cd[ax] >= 0 ? cd[ax] : LY::ND);
                 Real v[3];
                 if constexpr (ax < 3) {
                     mv3m<ZR, ZW>(Rpf, col[ax], v);
@@ -987,6 +998,12 @@ template <class T> struct DofTree {
         unsigned m = 1u << k;
         for (int j = par(k); j >= 0; j = par(j)) m |= 1u << j;
         return m;
+    }
+    /* dof 0 is on every dof's root path (phase 3's row stores rely on it) */
+    static constexpr bool root_common() {
+        for (int k = 0; k < T::ND; ++k)
+            if (!(path_mask(k) & 1u)) return false;
+        return true;
     }
 };
 
@@ -1399,7 +1416,7 @@ DEV Real pert_force(const PertArgs<Real> &P, double *sl, int k) {
  * m = lane + j*G.  h > 0: increment of the linearly-implicit substep;
  * h == 0: the true accelerations (realize).  Leaves coordinates, frames,
  * contact wrenches, limit forces and q'' (RHS slots) published in LDS. */
-template <class T, typename Real, bool PERT>
+template <class T, typename Real, bool PERT, bool BF_ROWS>
 DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Real ud,
                   const Real (&act)[Lay<T, Real>::MPL], const Real (&lce)[Lay<T, Real>::MPL],
                   const Real (&control)[Lay<T, Real>::MPL], int lane, Real *lds, Real h, bool equilibrate,
@@ -1460,15 +1477,19 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
         constexpr unsigned ICU = T::PLANAR ? 0x47u : 0x3FFu, WBU = T::PLANAR ? 0x1Cu : 0x3Fu;
         Real ic[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, wb[6] = {0, 0, 0, 0, 0, 0};
         if (lane < NB) {
+            /* planar: every body's record is read and weighted by 0 / 1 (lane
+             * an ancestor of d, or d): one basic block, the loads batch */
             sfor<0, NB>([&](auto dI) {
                 constexpr int d = decltype(dI)::value;
-                if ((T::anc[d] >> lane) & 1u) {
+                const bool mine = (T::anc[d] >> lane) & 1u;
+                if (T::PLANAR || mine) {
+                    const Real on = !T::PLANAR || mine ? Real(1) : Real(0);
 #pragma unroll
                     for (int i = 0; i < 10; ++i)
-                        if ((ICU >> i) & 1u) ic[i] += lds[LY::IC + 10 * d + i];
+                        if ((ICU >> i) & 1u) ic[i] = fma(on, lds[LY::IC + 10 * d + i], ic[i]);
 #pragma unroll
                     for (int i = 0; i < 6; ++i)
-                        if ((WBU >> i) & 1u) wb[i] += lds[LY::WB + 6 * d + i];
+                        if ((WBU >> i) & 1u) wb[i] = fma(on, lds[LY::WB + 6 * d + i], wb[i]);
                 }
             });
         }
@@ -1620,28 +1641,41 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
         });
         Real dg = 0;
 #pragma unroll
-        for (int li = 0; li < T::NL; ++li)
-            if (SM.lim_dof[li] == lane) { r += lds[LY::LIM + 4 * li + 2]; dg += lds[LY::LIM + 4 * li + 1]; }
+        for (int li = 0; li < T::NL; ++li) {   /* selects: no per-limit branch */
+            const bool mine = SM.lim_dof[li] == lane;
+            r += mine ? lds[LY::LIM + 4 * li + 2] : Real(0);
+            dg += mine ? lds[LY::LIM + 4 * li + 1] : Real(0);
+        }
         lds[LY::RHS + lane] = r;
-        /* dofs on k's root path, k included (compile-time per dof, selected by lane) */
-        unsigned path = 0;
-        sfor<0, ND>([&](auto kI) {
-            constexpr int k = decltype(kI)::value;
-            constexpr unsigned pm = DofTree<T>::path_mask(k);
-            path = lane == k ? pm : path;
-        });
+        /* Row k's entries (k, l), l <= k.  BF_ROWS: branch-free, every l is
+         * computed and stored in row k's own slots (those off k's root path
+         * are structural zeros ltl_solve never reads); columns l > k (not in
+         * row k) go to slot (k, 0) first, descending l, so the true (k, 0) —
+         * dof 0 is every dof's ancestor — is written last.  Same-box 2D
+         * 0.329 -> 0.316 ms, 3D 0.581 -> 0.561 (profiles/r03/ab_rows.txt).
+         * Otherwise only k's path entries, each under its own branch. */
+        static_assert(DofTree<T>::root_common(), "row stores park columns l > k in slot (k, 0)");
         Real *row = lds + LY::MP + (lane * (lane + 1)) / 2;
+        unsigned path = 0;   /* dofs on k's root path, k included (compile-time per dof, selected by lane) */
+        if constexpr (!BF_ROWS) {
+            sfor<0, ND>([&](auto kI) {
+                constexpr int k = decltype(kI)::value;
+                constexpr unsigned pm = DofTree<T>::path_mask(k);
+                path = lane == k ? pm : path;
+            });
+        }
         sfor<0, ND>([&](auto lI) {
-            constexpr int l = decltype(lI)::value;
-            if ((path >> l) & 1u) {
+            constexpr int l = ND - 1 - decltype(lI)::value;
+            auto entry = [&]() {
                 Real Sl[6];
 #pragma unroll
                 for (int i = 0; i < 6; ++i) Sl[i] = lds[LY::S + 6 * l + i];
                 PL::col(Sl);
                 Real v = dot3m<ZW, 0>(Sl, Gk) + dot3m<ZV, 0>(Sl + 3, Gk + 3);
-                if (implicit && l == lane) v += dg;
-                row[l] = v;
-            }
+                return v + (implicit && l == lane ? dg : Real(0));
+            };
+            if constexpr (BF_ROWS) row[l <= lane ? l : 0] = entry();
+            else if ((path >> l) & 1u) row[l] = entry();
         });
     }
     wave_sync();
@@ -2469,7 +2503,9 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                 pslot[0] = rk_t + cs * rk_h; pslot[1] = 0;
             }
             /* RK: explicit accelerations (h = 0, the implicit terms compile away) */
-            dynamics<T, Real, PERT>(*(const DModel<Real> *)Mi, SM, qd, ud, act, lce, control, lane, lds,
+            /* branch-free phase-3 row stores, except in the spatial RK kernels
+             * (they would take those kernels past the 512-register budget) */
+            dynamics<T, Real, PERT, !RK || T::PLANAR>(*(const DModel<Real> *)Mi, SM, qd, ud, act, lce, control, lane, lds,
                                     RK ? Real(0) : (sub ? dt : Real(0)), eq && NM > 0, PA, pslot,
                                     RK ? 0 : M.nsub - remaining, D);
         }
