@@ -246,6 +246,40 @@ DEV void fn_eval(const SModel<T, Real> &SM, int fi, Real q, Real &f, Real &f1, R
     }
 }
 
+/* fn_eval without branches (phase 0b's function slots): the spline is
+ * evaluated at the argument clamped to its knots (interval search and
+ * coefficients as in spline_eval) and the linear extrapolation, constant and
+ * linear kinds are selected; the same values as fn_eval, in one basic block
+ * so the slot's dependent LDS loads are not split by branches */
+template <class T, typename Real>
+DEV void fn_eval_bf(const SModel<T, Real> &SM, int fi, Real q, Real &f, Real &f1, Real &f2) {
+    const SFn<Real> &F = SM.fn[fi < 0 ? 0 : fi];
+    const int type = F.type, oo = F.off >= 0 ? F.off : 0, nn = F.n > 1 ? F.n : 1;
+    const Real a = F.a, b = F.b;
+    const Real x0 = SM.kx[oo], xn = SM.kx[oo + nn - 1];
+    const Real qc = q < x0 ? x0 : (q > xn ? xn : q);
+    int k = 0;
+#pragma unroll
+    for (int i = 1; i < T::NKMAX - 1; ++i) {
+        const Real xi = SM.kx[oo + (i < nn - 1 ? i : 0)];
+        k += (i < nn - 1 && qc > xi) ? 1 : 0;
+    }
+    const int j = oo + k, jn = oo + nn - 1;
+    const Real dx = qc - SM.kx[j], kb = SM.kb[j], kc = SM.kc[j], kd = SM.kd[j];
+    Real s0 = SM.ky[j] + dx * (kb + dx * (kc + dx * kd));
+    Real s1 = kb + dx * (Real(2) * kc + Real(3) * dx * kd);
+    Real s2 = Real(2) * kc + Real(6) * dx * kd;
+    const Real ylo = SM.ky[oo], blo = SM.kb[oo], yhi = SM.ky[jn], bhi = SM.kb[jn];
+    const bool lo = q < x0, hi = q > xn;
+    s0 = lo ? ylo + (q - x0) * blo : (hi ? yhi + (q - xn) * bhi : s0);
+    s1 = lo ? blo : (hi ? bhi : s1);
+    s2 = lo || hi ? Real(0) : s2;
+    const bool con = type == BIOIM_FN_CONST, lin = type == BIOIM_FN_LINEAR, present = fi >= 0;
+    f = !present ? Real(0) : (con ? b : (lin ? a * q + b : a * s0));
+    f1 = !present || con ? Real(0) : (lin ? a : a * s1);
+    f2 = !present || con || lin ? Real(0) : a * s2;
+}
+
 /* fn_eval specialised to the function kinds KM (bit kind+1; bit 0 = absent
  * axis) that can occur at this call site (compile-time, per topology axis) */
 template <unsigned KM, class T, typename Real>
@@ -855,13 +889,16 @@ template <class T, typename Real>
 DEV void fn_slots(const SModel<T, Real> &SM, Real *lds, int lane) {
     using LY = Lay<T, Real>;
     if constexpr (LY::NSLOT > 0) {
-        for (int f = lane; f < LY::NSLOT; f += T::G) {
-            Real v, d1, d2;
-            fn_eval<T, Real>(SM, SM.mf_fn[f], lds[LY::QF + SM.mf_coord[f]], v, d1, d2);
-            lds[LY::MF + 3 * f] = v;
-            lds[LY::MF + 3 * f + 1] = d1;
-            lds[LY::MF + 3 * f + 2] = d2;
-        }
+        sfor<0, (LY::NSLOT + T::G - 1) / T::G>([&](auto pI) {
+            const int f = lane + decltype(pI)::value * T::G;
+            if (f < LY::NSLOT) {
+                Real v, d1, d2;
+                fn_eval_bf<T, Real>(SM, SM.mf_fn[f], lds[LY::QF + SM.mf_coord[f]], v, d1, d2);
+                lds[LY::MF + 3 * f] = v;
+                lds[LY::MF + 3 * f + 1] = d1;
+                lds[LY::MF + 3 * f + 2] = d2;
+            }
+        });
         wave_sync();
     }
 }
@@ -1314,18 +1351,28 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
         }
     };
     const int npt = mu.npt;
-    sfor<0, (T::MAXPT > 0 ? T::MAXPT : 1)>([&](auto jI) {
+    constexpr int MP = T::MAXPT > 0 ? T::MAXPT : 1;
+    /* every slot's body and activity first (branch-free, slot 0 for slots
+     * past the count), so a point's frame loads wait on one LDS round trip
+     * inside its branch, not two */
+    int cbj[MP];
+    bool onj[MP];
+    sfor<0, MP>([&](auto jI) {
         constexpr int j = decltype(jI)::value;
-        if (j < npt) {
+        const DPathPt<Real> &pt = SM.pt[mu.pt_off + (j < npt ? j : 0)];
+        cbj[j] = pt.cbody;
+        onj[j] = j < npt;
+        if constexpr (((T::PT_COND >> j) & 1u) != 0) {
+            const bool cnd = pt.type == BIOIM_PT_COND;
+            const Real qc = ldsq[cnd ? pt.cond_coord : 0];
+            onj[j] = onj[j] && !(cnd && (qc < pt.lo || qc > pt.hi));
+        }
+    });
+    sfor<0, MP>([&](auto jI) {
+        constexpr int j = decltype(jI)::value;
+        {
             const DPathPt<Real> &pt = SM.pt[mu.pt_off + j];
-            bool on = true;
-            if constexpr (((T::PT_COND >> j) & 1u) != 0) {
-                if (pt.type == BIOIM_PT_COND) {
-                    Real qc = ldsq[pt.cond_coord];
-                    on = !(qc < pt.lo || qc > pt.hi);
-                }
-            }
-            if (on) {
+            if (onj[j]) {
                 Real loc[3] = {pt.loc[0], pt.loc[1], pt.loc[2]}, dloc[3] = {0, 0, 0};
                 if constexpr (((T::PT_MOVING >> j) & 1u) != 0) {
                     if (pt.type == BIOIM_PT_MOVING) {
@@ -1342,7 +1389,7 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
                         mv3(pt.R, dl, dloc);
                     }
                 }
-                const Real *kbp = lds + LY::KB + 18 * pt.cbody;
+                const Real *kbp = lds + LY::KB + 18 * cbj[j];
                 Real Rb[12];
 #pragma unroll
                 for (int i = 0; i < 12; ++i) Rb[i] = kbp[i];
