@@ -52,6 +52,18 @@ DEV void sfor(F &&f) {
     }
 }
 
+#ifndef BIOIM_ENV_MOD
+#define BIOIM_ENV_MOD -1
+#endif
+#ifndef BIOIM_BF_CURVE3D
+#define BIOIM_BF_CURVE3D 0
+#endif
+#ifndef BIOIM_BF_FV3D
+#define BIOIM_BF_FV3D 0
+#endif
+#ifndef BIOIM_BF_SPATIAL
+#define BIOIM_BF_SPATIAL 0
+#endif
 template <typename Real> struct Eps;
 template <> struct Eps<float> {
     static constexpr float u_tol = 2e-7f;   /* Bezier parameter tolerance  */
@@ -251,7 +263,7 @@ DEV void fn_eval(const SModel<T, Real> &SM, int fi, Real q, Real &f, Real &f1, R
  * coefficients as in spline_eval) and the linear extrapolation, constant and
  * linear kinds are selected; the same values as fn_eval, in one basic block
  * so the slot's dependent LDS loads are not split by branches */
-template <class T, typename Real>
+template <bool BFK, class T, typename Real>
 DEV void fn_eval_bf(const SModel<T, Real> &SM, int fi, Real q, Real &f, Real &f1, Real &f2) {
     const SFn<Real> &F = SM.fn[fi < 0 ? 0 : fi];
     const int type = F.type, oo = F.off >= 0 ? F.off : 0, nn = F.n > 1 ? F.n : 1;
@@ -271,13 +283,27 @@ DEV void fn_eval_bf(const SModel<T, Real> &SM, int fi, Real q, Real &f, Real &f1
     Real s2 = Real(2) * kc + Real(6) * dx * kd;
     const Real ylo = SM.ky[oo], blo = SM.kb[oo], yhi = SM.ky[jn], bhi = SM.kb[jn];
     const bool lo = q < x0, hi = q > xn;
-    s0 = lo ? ylo + (q - x0) * blo : (hi ? yhi + (q - xn) * bhi : s0);
-    s1 = lo ? blo : (hi ? bhi : s1);
-    s2 = lo || hi ? Real(0) : s2;
+    /* every ?: below picks between plain locals: clang emits a ?: whose arms
+     * are expressions as a branch, the loads feeding an arm then sink into
+     * it and the branch can no longer be folded into a select */
     const bool con = type == BIOIM_FN_CONST, lin = type == BIOIM_FN_LINEAR, present = fi >= 0;
-    f = !present ? Real(0) : (con ? b : (lin ? a * q + b : a * s0));
-    f1 = !present || con ? Real(0) : (lin ? a : a * s1);
-    f2 = !present || con || lin ? Real(0) : a * s2;
+    if constexpr (BFK) {
+        const Real elo = ylo + (q - x0) * blo, ehi = yhi + (q - xn) * bhi, zero = 0;
+        s0 = lo ? elo : (hi ? ehi : s0);
+        s1 = lo ? blo : (hi ? bhi : s1);
+        s2 = lo || hi ? zero : s2;
+        const Real vl = a * q + b, vs = a * s0, vs1 = a * s1, vs2 = a * s2;
+        f = !present ? zero : (con ? b : (lin ? vl : vs));
+        f1 = !present || con ? zero : (lin ? a : vs1);
+        f2 = !present || con || lin ? zero : vs2;
+    } else {
+        s0 = lo ? ylo + (q - x0) * blo : (hi ? yhi + (q - xn) * bhi : s0);
+        s1 = lo ? blo : (hi ? bhi : s1);
+        s2 = lo || hi ? Real(0) : s2;
+        f = !present ? Real(0) : (con ? b : (lin ? a * q + b : a * s0));
+        f1 = !present || con ? Real(0) : (lin ? a : a * s1);
+        f2 = !present || con || lin ? Real(0) : a * s2;
+    }
 }
 
 /* fn_eval specialised to the function kinds KM (bit kind+1; bit 0 = absent
@@ -396,7 +422,7 @@ template <typename Real> DEV Real dbez5(const Real *c, Real u) {
  * then Newton steps on the quintic x(u): two reach machine precision in
  * fp64, one is below fp32 rounding (tests/test_curves.py); linear
  * extrapolation outside [x0, x1]. */
-template <typename Real>
+template <bool BF = true, typename Real>
 DEV void curve_eval(const DCurve<Real> &C, Real x, Real &y, Real &dydx) {
     Real xc = x < C.x0 ? C.x0 : (x > C.x1 ? C.x1 : x);
     int k = 0;
@@ -418,8 +444,20 @@ DEV void curve_eval(const DCurve<Real> &C, Real x, Real &y, Real &dydx) {
     for (int it = 0; it < Eps<Real>::curve_newton; ++it) u -= (bez5(px, u) - xc) * newton_rcp(dbez5(px, u));
     y = bez5(py, u);
     dydx = dbez5(py, u) * fast_rcp(dbez5(px, u));
-    if (x < C.x0) { y = C.y0 + C.dydx0 * (x - C.x0); dydx = C.dydx0; }
-    if (x > C.x1) { y = C.y1 + C.dydx1 * (x - C.x1); dydx = C.dydx1; }
+    /* linear extrapolation blended in by 0 / 1 weights (every term finite):
+     * a load under the condition, or a select of loaded values, made the
+     * compiler branch, which split the muscle eval's three independent curve
+     * chains into separate basic blocks */
+    if constexpr (BF) {
+        const Real x0 = C.x0, y0 = C.y0, d0 = C.dydx0, x1 = C.x1, y1 = C.y1, d1 = C.dydx1;
+        const Real ylo = y0 + d0 * (x - x0), yhi = y1 + d1 * (x - x1);
+        const Real wb = x < x0 ? Real(1) : Real(0), wa = x > x1 ? Real(1) : Real(0), wm = Real(1) - wb - wa;
+        y = fma(wb, ylo, fma(wa, yhi, wm * y));
+        dydx = fma(wb, d0, fma(wa, d1, wm * dydx));
+    } else {   /* the branching form: separate blocks, fewer values live at once */
+        if (x < C.x0) { y = C.y0 + C.dydx0 * (x - C.x0); dydx = C.dydx0; }
+        if (x > C.x1) { y = C.y1 + C.dydx1 * (x - C.x1); dydx = C.dydx1; }
+    }
 }
 
 /* root of a*fal*fv(v) + beta*v = rhs (strictly increasing in v), solved in the
@@ -427,7 +465,7 @@ DEV void curve_eval(const DCurve<Real> &C, Real x, Real &y, Real &dydx) {
  * previous substep's root) through the segment's u(x) table; returns v, fv,
  * dfv/dv.  At least two safeguarded Newton steps, then more until
  * converged. */
-template <typename Real>
+template <bool BF = true, typename Real>
 DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0, Real &v, Real &fv, Real &dfv) {
     Real g0 = afal * C.y0 + beta * C.x0 - rhs;
     Real g1 = afal * C.y1 + beta * C.x1 - rhs;
@@ -439,17 +477,32 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
     for (int i = 0; i < 6; ++i) { px[i] = C.cx[k][i]; py[i] = C.cy[k][i]; }
     const Real xa = C.xa[k], xb = C.xb[k];
     Real ga = afal * C.ya[k] + beta * xa - rhs, gb = afal * C.yb[k] + beta * xb - rhs;
+    /* both starts computed, one selected (no branch: the table loads and the
+     * division stay in the muscle eval's basic block) — the warm start
+     * through the segment's u(x) table, or the secant of g over the segment */
     Real u;
-    if (v0 > xa && v0 < xb) {
-        Real tt = (v0 - xa) * C.inv_h[k];
+    if constexpr (!BF) {
+        if (v0 > xa && v0 < xb) {
+            Real tt = (v0 - xa) * C.inv_h[k];
+            int i0 = (int)tt;
+            i0 = i0 < 0 ? 0 : (i0 > BIOIM_UTAB - 1 ? BIOIM_UTAB - 1 : i0);
+            Real fr = tt - Real(i0);
+            u = C.ut[k][i0] + fr * (C.ut[k][i0 + 1] - C.ut[k][i0]);
+        } else {
+            u = ga / (ga - gb);
+        }
+    } else {
+        const Real vc = v0 > xa ? (v0 < xb ? v0 : xb) : xa;
+        Real tt = (vc - xa) * C.inv_h[k];
         int i0 = (int)tt;
         i0 = i0 < 0 ? 0 : (i0 > BIOIM_UTAB - 1 ? BIOIM_UTAB - 1 : i0);
         Real fr = tt - Real(i0);
-        u = C.ut[k][i0] + fr * (C.ut[k][i0 + 1] - C.ut[k][i0]);
-    } else {
-        u = ga / (ga - gb);
+        const Real ua = C.ut[k][i0], ub = C.ut[k][i0 + 1];
+        const Real ut = ua + fr * (ub - ua), us = ga / (ga - gb);
+        u = ((v0 > xa) & (v0 < xb)) ? ut : us;
     }
-    u = u > Real(0) && u < Real(1) ? u : Real(0.5);
+    const Real half = 0.5;
+    u = ((u > Real(0)) & (u < Real(1))) ? u : half;
     /* g(u) = a fal y(u) + beta x(u) - rhs is one quintic in u */
     Real pg[6];
 #pragma unroll
@@ -482,12 +535,22 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
     v = bez5(px, u);
     fv = bez5(py, u);
     dfv = dbez5(py, u) * fast_rcp(dbez5(px, u));
-    if (g0 >= 0) {
-        v = (rhs - afal * (C.y0 - C.dydx0 * C.x0)) / (afal * C.dydx0 + beta);
-        fv = C.y0 + C.dydx0 * (v - C.x0); dfv = C.dydx0;
-    } else if (g1 <= 0) {
-        v = (rhs - afal * (C.y1 - C.dydx1 * C.x1)) / (afal * C.dydx1 + beta);
-        fv = C.y1 + C.dydx1 * (v - C.x1); dfv = C.dydx1;
+    if constexpr (!BF) {
+        if (g0 >= 0) {
+            v = (rhs - afal * (C.y0 - C.dydx0 * C.x0)) / (afal * C.dydx0 + beta);
+            fv = C.y0 + C.dydx0 * (v - C.x0); dfv = C.dydx0;
+        } else if (g1 <= 0) {
+            v = (rhs - afal * (C.y1 - C.dydx1 * C.x1)) / (afal * C.dydx1 + beta);
+            fv = C.y1 + C.dydx1 * (v - C.x1); dfv = C.dydx1;
+        }
+    } else {   /* linear extrapolation past an end (one division, selected) */
+        const Real y0 = C.y0, d0 = C.dydx0, x0 = C.x0, y1 = C.y1, d1 = C.dydx1, x1 = C.x1;
+        const bool e0 = g0 >= 0, e1 = g1 <= 0;
+        const Real yE = e0 ? y0 : y1, dE = e0 ? d0 : d1, xE = e0 ? x0 : x1;
+        const Real vE = (rhs - afal * (yE - dE * xE)) / (afal * dE + beta);
+        const Real fvE = yE + dE * (vE - xE);
+        const bool ext = e0 | e1;
+        v = ext ? vE : v; fv = ext ? fvE : fv; dfv = ext ? dE : dfv;
     }
 }
 
@@ -550,7 +613,12 @@ template <class T, typename Real> struct Lay {
     static constexpr int U1 = 24 * (NB + 1) + 6 * (ND + 1), U2 = TAUN + NS * CJN;
     static constexpr int U3 = OBSMAX + 6 * (T::NOS + 1);
     static constexpr int USZ = U1 > U2 ? (U1 > U3 ? U1 : U3) : (U2 > U3 ? U2 : U3);
-    static constexpr int SIZE = ((U + USZ + 1) / 2) * 2;
+    static constexpr int SIZE0 = ((U + USZ + 1) / 2) * 2;
+    /* per-env stride residue mod 32 doubles (BIOIM_ENV_MOD >= 0, planar
+     * topologies; the spatial ones have no LDS to spare): it sets which banks
+     * the other env of a 32-lane group hits (ds_read_b64: 2 x 32 lanes;
+     * ds_read_b128: 16-lane groups mixing both envs) */
+    static constexpr int SIZE = (BIOIM_ENV_MOD >= 0 && T::PLANAR) ? SIZE0 + ((BIOIM_ENV_MOD - SIZE0 % 32) + 32) % 32 : SIZE0;
 };
 
 /* apply_perturbations kernels only: per env 5 doubles after all env regions
@@ -885,7 +953,7 @@ DEV void kin_chain(const SModel<T, Real> &SM, Real *lds, int c, Real x0) {
 /* Phase 0b: the function slots (Lay::MF), one lane each — moving path
  * points' location functions and the joints' spline axes — from the
  * published coordinates; ends with a wave sync when there are any */
-template <class T, typename Real>
+template <bool BFK, class T, typename Real>
 DEV void fn_slots(const SModel<T, Real> &SM, Real *lds, int lane) {
     using LY = Lay<T, Real>;
     if constexpr (LY::NSLOT > 0) {
@@ -893,7 +961,7 @@ DEV void fn_slots(const SModel<T, Real> &SM, Real *lds, int lane) {
             const int f = lane + decltype(pI)::value * T::G;
             if (f < LY::NSLOT) {
                 Real v, d1, d2;
-                fn_eval_bf<T, Real>(SM, SM.mf_fn[f], lds[LY::QF + SM.mf_coord[f]], v, d1, d2);
+                fn_eval_bf<BFK, T, Real>(SM, SM.mf_fn[f], lds[LY::QF + SM.mf_coord[f]], v, d1, d2);
                 lds[LY::MF + 3 * f] = v;
                 lds[LY::MF + 3 * f + 1] = d1;
                 lds[LY::MF + 3 * f + 2] = d2;
@@ -1093,16 +1161,24 @@ template <class T, int N, typename Real> DEV bool ltl_solve(Real *A, Real *b) {
 }
 
 /* ---------------------------------------------------- contact + limits */
-template <typename Real> DEV Real smooth_step(Real y0, Real y1, Real x0, Real x1, Real iw, Real x) {
-    if (x <= x0) return y0;
-    if (x >= x1) return y1;
+/* branch-free: the transition polynomial is evaluated everywhere and
+ * selected (finite for any x) */
+template <bool BF, typename Real> DEV Real smooth_step(Real y0, Real y1, Real x0, Real x1, Real iw, Real x) {
+    if constexpr (!BF) {
+        if (x <= x0) return y0;
+        if (x >= x1) return y1;
+    }
     Real t = (x - x0) * iw;   /* iw = 1 / (x1 - x0) */
-    return y0 + (y1 - y0) * t * t * t * (Real(10) + t * (Real(6) * t - Real(15)));
+    const Real v = y0 + (y1 - y0) * t * t * t * (Real(10) + t * (Real(6) * t - Real(15)));
+    return x <= x0 ? y0 : (x >= x1 ? y1 : v);
 }
-template <typename Real> DEV Real smooth_step_d(Real y0, Real y1, Real x0, Real x1, Real iw, Real x) {
-    if (x <= x0 || x >= x1) return 0;
+template <bool BF, typename Real> DEV Real smooth_step_d(Real y0, Real y1, Real x0, Real x1, Real iw, Real x) {
+    if constexpr (!BF) {
+        if (x <= x0 || x >= x1) return 0;
+    }
     Real t = (x - x0) * iw;
-    return (y1 - y0) * Real(30) * t * t * (Real(1) - t) * (Real(1) - t) * iw;
+    const Real v = (y1 - y0) * Real(30) * t * t * (Real(1) - t) * (Real(1) - t) * iw, zero = 0;
+    return ((x <= x0) | (x >= x1)) ? zero : v;
 }
 
 /* Hunt-Crossley sphere s (this lane) vs the ground plane.  Publishes the
@@ -1122,7 +1198,7 @@ template <typename Real> DEV Real smooth_step_d(Real y0, Real y1, Real x0, Real 
 template <typename Real> struct ContactOut {
     Real cw[7], cj[10];
 };
-template <class T, typename Real>
+template <bool BFK, class T, typename Real>
 DEV void contact_compute(const SModel<T, Real> &SM, const Real *lds, int s, Real h, ContactOut<Real> &o) {
     using LY = Lay<T, Real>;
     using PL = Planar<T>;
@@ -1147,14 +1223,28 @@ DEV void contact_compute(const SModel<T, Real> &SM, const Real *lds, int s, Real
     PL::lin(vs);
     const Real vn = -vs[1];
     const Real kk = SM.cf_kk[fo], cc = SM.cf_c[fo];
-    const Real dps = pen ? depth : Real(1);
+    const Real dps = pen ? depth : Real(1), zero = 0;
     const Real rkd = rad * kk * dps;
-    const Real fH = pen ? Real(4.0 / 3.0) * kk * dps * (rkd * fast_rsqrt(rkd)) : Real(0);
+    /* ?: arms are plain locals: an expression arm makes clang emit a branch */
+    constexpr bool BF = BFK;
+    Real fH;
+    if constexpr (BF) {
+        const Real fHp = Real(4.0 / 3.0) * kk * dps * (rkd * fast_rsqrt(rkd));
+        fH = pen ? fHp : zero;
+    } else {
+        fH = pen ? Real(4.0 / 3.0) * kk * dps * (rkd * fast_rsqrt(rkd)) : Real(0);
+    }
     const Real fn = fH * (Real(1) + Real(1.5) * cc * vn);
     const bool active = pen && fn > 0;
     const Real vt0 = -vs[0], vt2 = -vs[2];
     const Real vs2 = vt0 * vt0 + vt2 * vt2;
-    const Real ivs = vs2 > 0 ? fast_rsqrt(vs2) : Real(0);
+    Real ivs;
+    if constexpr (BF) {
+        const Real rvs = fast_rsqrt(vs2);
+        ivs = vs2 > 0 ? rvs : zero;
+    } else {
+        ivs = vs2 > 0 ? fast_rsqrt(vs2) : Real(0);
+    }
     const Real vslip = vs2 * ivs;
     const Real vtr = SM.cf_vt[fo], ms = SM.cf_ms[fo], md = SM.cf_md[fo], mv = SM.cf_mv[fo];
     const Real ivtr = fast_rcp(vtr);
@@ -1162,7 +1252,13 @@ DEV void contact_compute(const SModel<T, Real> &SM, const Real *lds, int s, Real
     const Real iden = fast_rcp(den);
     const Real ff = fn * (fmin(r_, Real(1)) * (md + Real(2) * (ms - md) * iden) + mv * vslip);
     const bool slip = vslip != 0;
-    Real F[3] = {slip ? ff * vt0 * ivs : Real(0), fn, slip ? ff * vt2 * ivs : Real(0)};
+    Real F[3];
+    if constexpr (BF) {
+        const Real fx = ff * vt0 * ivs, fz = ff * vt2 * ivs;
+        F[0] = slip ? fx : zero; F[1] = fn; F[2] = slip ? fz : zero;
+    } else {
+        F[0] = slip ? ff * vt0 * ivs : Real(0); F[1] = fn; F[2] = slip ? ff * vt2 * ivs : Real(0);
+    }
     Real mo[3];
     cross3(P, F, mo);
 #pragma unroll
@@ -1197,10 +1293,10 @@ template <class T, typename Real> DEV void contact_store(Real *lds, int s, const
 #pragma unroll
     for (int i = 0; i < 10; ++i) cj[i] = o.cj[i];
 }
-template <class T, typename Real>
+template <bool BFK, class T, typename Real>
 DEV void contact_lane(const SModel<T, Real> &SM, Real *lds, int s, Real h) {
     ContactOut<Real> o;
-    contact_compute<T, Real>(SM, lds, s, h, o);
+    contact_compute<BFK, T, Real>(SM, lds, s, h, o);
     contact_store<T, Real>(lds, s, o);
 }
 
@@ -1217,33 +1313,55 @@ template <typename Real> struct MState {
     bool clamped;
 };
 
-template <class T, typename Real>
+template <bool BFK, class T, typename Real>
 DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_state, Real l_state, Real excitation,
                      Real L, Real v_warm, MState<Real> &s) {
     STAMP_DECL
     const DCurve<Real> &Cfal = SM.curve[mu.cv[0]], &Cfv = SM.curve[mu.cv[1]], &Cfpe = SM.curve[mu.cv[2]],
                        &Cfse = SM.curve[mu.cv[3]];
-    Real a = a_state < mu.amin ? mu.amin : (a_state > Real(1) ? Real(1) : a_state);
-    Real lce = l_state < mu.lmin ? mu.lmin : l_state;
+    /* ?: arms are plain locals throughout (see below) */
+    constexpr bool BF = BFK;
+    const Real amin = mu.amin, lmin = mu.lmin, one = 1, zero = 0;
+    Real a, lce;
+    if constexpr (BF) {
+        a = a_state < amin ? amin : (a_state > one ? one : a_state);
+        lce = l_state < lmin ? lmin : l_state;
+    } else {
+        a = a_state < mu.amin ? mu.amin : (a_state > Real(1) ? Real(1) : a_state);
+        lce = l_state < mu.lmin ? mu.lmin : l_state;
+    }
     Real w = mu.width;
     const Real sq2 = lce * lce - w * w;
     const Real isq = fast_rsqrt(sq2), sq = sq2 * isq;
     const Real icos = lce * isq;          /* 1 / cos(pennation) */
     Real lt = L - sq;
     Real fse, dfse, fal, dfal, fpe, dfpe;
-    curve_eval(Cfse, lt * mu.inv_lts, fse, dfse);
-    curve_eval(Cfal, lce * mu.inv_lopt, fal, dfal);
-    curve_eval(Cfpe, lce * mu.inv_lopt, fpe, dfpe);
+    /* BF: the three curve chains and the fiber-velocity start in one basic
+     * block (planar kernels; the spatial fp64 kernels, two muscles per lane,
+     * would spill) */
+    curve_eval<BF || BIOIM_BF_CURVE3D>(Cfse, lt * mu.inv_lts, fse, dfse);
+    curve_eval<BF || BIOIM_BF_CURVE3D>(Cfal, lce * mu.inv_lopt, fal, dfal);
+    curve_eval<BF || BIOIM_BF_CURVE3D>(Cfpe, lce * mu.inv_lopt, fpe, dfpe);
     Real rhs = fse * icos - fpe;
     STAMP(16);
     Real vN, fvv, dfv;
-    solve_fv(Cfv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
+    solve_fv<BF || BIOIM_BF_FV3D>(Cfv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
     STAMP(17);
     Real dGdv = a * fal * dfv + mu.beta;
-    bool clamped = (l_state <= mu.lmin && vN <= 0) || l_state < mu.lmin;
-    if (clamped) {
-        vN = 0;
-        fvv = Cfv.y_at0;
+    /* selects over plain locals (a load in a ?: arm or an if body becomes a
+     * branch that splits the muscle eval's basic block) */
+    bool clamped;
+    if constexpr (BF) {
+        const Real fv_at0 = Cfv.y_at0;
+        clamped = ((l_state <= lmin) & (vN <= 0)) | (l_state < lmin);
+        vN = clamped ? zero : vN;
+        fvv = clamped ? fv_at0 : fvv;
+    } else {
+        clamped = (l_state <= mu.lmin && vN <= 0) || l_state < mu.lmin;
+        if (clamped) {
+            vN = 0;
+            fvv = Cfv.y_at0;
+        }
     }
     s.act = a;
     s.lce = lce;
@@ -1254,16 +1372,25 @@ DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_
     s.Ff = mu.fiso * (a * fal * fvv + fpe + mu.beta * vN);
     s.clamped = clamped;
     Real dGdl = (a * dfal * fvv + dfpe) * mu.inv_lopt + dfse * mu.inv_lts * (icos * icos) + fse * w * w * (isq * isq * isq);
-    s.dvdl = clamped ? Real(0) : -(dGdl * fast_rcp(dGdv)) * mu.lv;
-    Real u = excitation < mu.amin ? mu.amin : (excitation > Real(1) ? Real(1) : excitation);
-    const Real ab = Real(0.5) + Real(1.5) * a;
-    /* du/dt = (u - a) / tau, tau = tau_act (0.5 + 1.5 a) or tau_deact / (0.5 + 1.5 a) */
-    s.dadt = u > a ? (u - a) * fast_rcp(mu.tau_act * ab) : (u - a) * ab * fast_rcp(mu.tau_deact);
+    if constexpr (BF) {
+        const Real dvdl = -(dGdl * fast_rcp(dGdv)) * mu.lv;
+        s.dvdl = clamped ? zero : dvdl;
+        Real u = excitation < amin ? amin : (excitation > one ? one : excitation);
+        const Real ab = Real(0.5) + Real(1.5) * a;
+        /* du/dt = (u - a) / tau, tau = tau_act (0.5 + 1.5 a) or tau_deact / (0.5 + 1.5 a) */
+        const Real da_act = (u - a) * fast_rcp(mu.tau_act * ab), da_deact = (u - a) * ab * fast_rcp(mu.tau_deact);
+        s.dadt = u > a ? da_act : da_deact;
+    } else {
+        s.dvdl = clamped ? Real(0) : -(dGdl * fast_rcp(dGdv)) * mu.lv;
+        Real u = excitation < mu.amin ? mu.amin : (excitation > Real(1) ? Real(1) : excitation);
+        const Real ab = Real(0.5) + Real(1.5) * a;
+        s.dadt = u > a ? (u - a) * fast_rcp(mu.tau_act * ab) : (u - a) * ab * fast_rcp(mu.tau_deact);
+    }
     STAMP(18);
 }
 
 /* static fiber equilibrium at reset (zero fiber velocity) */
-template <class T, typename Real>
+template <bool BFK, class T, typename Real>
 DEV Real muscle_equilibrium(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_state, Real L) {
     const DCurve<Real> &Cfal = SM.curve[mu.cv[0]], &Cfpe = SM.curve[mu.cv[2]], &Cfse = SM.curve[mu.cv[3]];
     Real a = a_state < mu.amin ? mu.amin : (a_state > Real(1) ? Real(1) : a_state);
@@ -1272,9 +1399,9 @@ DEV Real muscle_equilibrium(const SModel<T, Real> &SM, const SMuscle<Real> &mu, 
     if (!(L - mu.lts > sqrt(lo * lo - w * w))) return lo;
     {   /* the fiber out-pulls the tendon even at its minimum length: no root */
         Real sq = sqrt(lo * lo - w * w), fal, dfal, fpe, dfpe, fse, dfse;
-        curve_eval(Cfal, lo * mu.inv_lopt, fal, dfal);
-        curve_eval(Cfpe, lo * mu.inv_lopt, fpe, dfpe);
-        curve_eval(Cfse, (L - sq) * mu.inv_lts, fse, dfse);
+        curve_eval<BFK>(Cfal, lo * mu.inv_lopt, fal, dfal);
+        curve_eval<BFK>(Cfpe, lo * mu.inv_lopt, fpe, dfpe);
+        curve_eval<BFK>(Cfse, (L - sq) * mu.inv_lts, fse, dfse);
         if ((a * fal + fpe) * (sq / lo) - fse >= 0) return lo;
     }
     Real l = sqrt((L - Real(1.01) * mu.lts) * (L - Real(1.01) * mu.lts) + w * w), dprev = 1;
@@ -1282,9 +1409,9 @@ DEV Real muscle_equilibrium(const SModel<T, Real> &SM, const SMuscle<Real> &mu, 
     for (int it = 0; it < 4 * Eps<Real>::it_max; ++it) {
         Real sq = sqrt(l * l - w * w), cphi = sq / l;
         Real fal, dfal, fpe, dfpe, fse, dfse;
-        curve_eval(Cfal, l * mu.inv_lopt, fal, dfal);
-        curve_eval(Cfpe, l * mu.inv_lopt, fpe, dfpe);
-        curve_eval(Cfse, (L - sq) * mu.inv_lts, fse, dfse);
+        curve_eval<BFK>(Cfal, l * mu.inv_lopt, fal, dfal);
+        curve_eval<BFK>(Cfpe, l * mu.inv_lopt, fpe, dfpe);
+        curve_eval<BFK>(Cfse, (L - sq) * mu.inv_lts, fse, dfse);
         Real H = (a * fal + fpe) * cphi - fse;
         Real dH = (a * dfal + dfpe) * mu.inv_lopt * cphi + (a * fal + fpe) * (w * w) / (l * l * sq) + dfse * mu.inv_lts / cphi;
         if (H > 0) hi = l; else lo = l;
@@ -1313,13 +1440,14 @@ DEV Real muscle_equilibrium(const SModel<T, Real> &SM, const SMuscle<Real> &mu, 
  * coordinate.  The floating-base dofs are skipped: their sum over a path is
  * zero (sum g = 0, sum P x g = 0).  The span's Plucker columns are read from
  * LDS once per muscle into registers. */
-template <class T, typename Real>
+template <bool BFK, class T, typename Real>
 DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const Real *lds, Real &L,
                      Real (&dLs)[T::MAXSPAN]) {
     using LY = Lay<T, Real>;
     using PL = Planar<T>;
     constexpr unsigned ZR = PL::ZR, ZW = PL::ZW, ZV = PL::ZV;
     constexpr int NSP = T::MAXSPAN;
+    constexpr bool BF = BFK;
     const Real *ldsq = lds + LY::QF;
     L = 0;
     int sd[NSP];
@@ -1327,8 +1455,19 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
 #pragma unroll
     for (int k = 0; k < NSP; ++k) {
         dLs[k] = 0;
-        sd[k] = k < mu.nspan ? mu.span[k] : -1;
-        const int dk = k < mu.nspan ? mu.span[k] : 0;
+        /* planar: ?: over plain locals only (an arm with a load becomes a
+         * branch); the spatial kernels keep the branches (fewer live values
+         * in their two muscle passes) */
+        int dk;
+        if constexpr (BF) {
+            const int spk = mu.span[k], none = -1, zero = 0;
+            const bool ink = k < mu.nspan;
+            sd[k] = ink ? spk : none;
+            dk = ink ? spk : zero;
+        } else {
+            sd[k] = k < mu.nspan ? mu.span[k] : -1;
+            dk = k < mu.nspan ? mu.span[k] : 0;
+        }
 #pragma unroll
         for (int i = 0; i < 6; ++i) Ss[k][i] = lds[LY::S + 6 * dk + i];
         PL::col(Ss[k]);
@@ -1364,8 +1503,14 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
         onj[j] = j < npt;
         if constexpr (((T::PT_COND >> j) & 1u) != 0) {
             const bool cnd = pt.type == BIOIM_PT_COND;
-            const Real qc = ldsq[cnd ? pt.cond_coord : 0];
-            onj[j] = onj[j] && !(cnd && (qc < pt.lo || qc > pt.hi));
+            if constexpr (BF) {
+                const int ccd = pt.cond_coord, zero = 0;
+                const Real qc = ldsq[cnd ? ccd : zero], plo = pt.lo, phi = pt.hi;
+                onj[j] = onj[j] & !(cnd & ((qc < plo) | (qc > phi)));   /* no short-circuit branches */
+            } else {
+                const Real qc = ldsq[cnd ? pt.cond_coord : 0];
+                onj[j] = onj[j] && !(cnd && (qc < pt.lo || qc > pt.hi));
+            }
         }
     });
     sfor<0, MP>([&](auto jI) {
@@ -1380,8 +1525,15 @@ DEV void muscle_path(const SModel<T, Real> &SM, const SMuscle<Real> &mu, const R
 #pragma unroll
                         for (int a = 0; a < 3; ++a) {
                             const int f = pt.mf[a];
-                            ll[a] = f < 0 ? pt.loc[a] : lds[LY::MF + 3 * (f < 0 ? 0 : f)];
-                            dl[a] = f < 0 ? Real(0) : lds[LY::MF + 3 * (f < 0 ? 0 : f) + 1];
+                            if constexpr (BF) {
+                                const Real l0 = pt.loc[a], fv = lds[LY::MF + 3 * (f < 0 ? 0 : f)],
+                                           fd = lds[LY::MF + 3 * (f < 0 ? 0 : f) + 1], zero = 0;
+                                ll[a] = f < 0 ? l0 : fv;
+                                dl[a] = f < 0 ? zero : fd;
+                            } else {
+                                ll[a] = f < 0 ? pt.loc[a] : lds[LY::MF + 3 * (f < 0 ? 0 : f)];
+                                dl[a] = f < 0 ? Real(0) : lds[LY::MF + 3 * (f < 0 ? 0 : f) + 1];
+                            }
                         }
                         mv3(pt.R, ll, loc);
 #pragma unroll
@@ -1463,7 +1615,7 @@ DEV Real pert_force(const PertArgs<Real> &P, double *sl, int k) {
  * m = lane + j*G.  h > 0: increment of the linearly-implicit substep;
  * h == 0: the true accelerations (realize).  Leaves coordinates, frames,
  * contact wrenches, limit forces and q'' (RHS slots) published in LDS. */
-template <class T, typename Real, bool PERT, bool BF_ROWS>
+template <class T, typename Real, bool PERT, bool BF_ROWS, bool IMP>
 DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Real ud,
                   const Real (&act)[Lay<T, Real>::MPL], const Real (&lce)[Lay<T, Real>::MPL],
                   const Real (&control)[Lay<T, Real>::MPL], int lane, Real *lds, Real h, bool equilibrate,
@@ -1471,6 +1623,16 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     using LY = Lay<T, Real>;
     constexpr int ND = LY::ND, NP = LY::NP, NB = T::NB, G = T::G, MPL = LY::MPL;
     static_assert(NB < G && ND <= G, "lane NB writes the ground slot; one lane per dof");
+    /* the semi-implicit planar kernels: the implicit contact / limit terms
+     * without a branch on h (the spatial kernels keep it: register budget) */
+    constexpr bool IMP_BF = IMP && (T::PLANAR || BIOIM_BF_SPATIAL);
+    /* the branch-free forms (selects over plain locals, blended
+     * extrapolations, one basic block per muscle eval) in the semi-implicit
+     * planar kernels only: the RK kernels keep the round-2 code, whose
+     * register allocation is GPU-verified (an RK build of these forms put a
+     * lane-divergent copy of a live-in-all-lanes address into an AGPR and
+     * faulted) */
+    constexpr bool BFK = IMP_BF;
     STAMP_DECL
     publish_coords<T, Real>(M, SM, lds, lane, qd, ud);
     if (lane < ND) {
@@ -1487,7 +1649,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     /* ---- phase 0b: function slots, one lane each — the moving path points'
      * location functions (read by every muscle that has the point) and the
      * joints' spline axes (read by their body's lane) */
-    fn_slots<T, Real>(SM, lds, lane);
+    fn_slots<BFK, T, Real>(SM, lds, lane);
     STAMP(15);
 
     /* ---- phase 1: lane-parallel kinematics */
@@ -1569,19 +1731,19 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
             if (m < T::NM) {
                 const SMuscle<Real> &mu = SM.mus[m];
                 Real L, dLs[T::MAXSPAN];
-                muscle_path<T, Real>(SM, mu, lds, L, dLs);
+                muscle_path<BFK, T, Real>(SM, mu, lds, L, dLs);
                 STAMP(4);
                 Real a_ = act[j], l_ = lce[j];
                 if (equilibrate) /* equilibrateMuscles: static fiber equilibrium at the held activation
                                   * (a reset has set the default activation) */
-                    l_ = muscle_equilibrium<T, Real>(SM, mu, a_, L);
+                    l_ = muscle_equilibrium<BFK, T, Real>(SM, mu, a_, L);
                 D.act[j] = a_;
                 D.lce[j] = l_;
                 /* the sphere contacts ride in the first muscle pass (every
                  * sphere lane holds a muscle): same block as the curve
                  * evaluations, so their chains interleave */
-                if constexpr (j == 0 && MUSCLE_CONTACT) contact_compute<T, Real>(SM, lds, lane < T::NS ? lane : 0, h, CO);
-                muscle_eval<T, Real>(SM, mu, a_, l_, control[j], L, D.ms[j].vN, D.ms[j]);
+                if constexpr (j == 0 && MUSCLE_CONTACT) contact_compute<BFK, T, Real>(SM, lds, lane < T::NS ? lane : 0, h, CO);
+                muscle_eval<BFK, T, Real>(SM, mu, a_, l_, control[j], L, D.ms[j].vN, D.ms[j]);
                 const Real nFt = -D.ms[j].Ft;
                 Real *ts = lds + LY::TAU + (lane + j * G) * T::MAXSPAN;
 #pragma unroll
@@ -1601,20 +1763,20 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     if constexpr (MUSCLE_CONTACT) {
         if (lane < T::NS) contact_store<T, Real>(lds, lane, CO);
     } else {
-        if (lane < T::NS) contact_lane<T, Real>(SM, lds, lane, h);
+        if (lane < T::NS) contact_lane<BFK, T, Real>(SM, lds, lane, h);
     }
     STAMP(6);
     if (lane < T::NL) {
         int cc = SM.lim_coord[lane];
         Real qv = lds[LY::QF + cc], qd = lds[LY::UF + cc];
         Real qup = SM.lim_qup[lane], qlo = SM.lim_qlow[lane], tr = SM.lim_trans[lane], itr = SM.lim_itrans[lane];
-        Real up = smooth_step(Real(0), Real(1), qup, qup + tr, itr, qv);
-        Real lo = smooth_step(Real(1), Real(0), qlo - tr, qlo, itr, qv);
+        Real up = smooth_step<BFK>(Real(0), Real(1), qup, qup + tr, itr, qv);
+        Real lo = smooth_step<BFK>(Real(1), Real(0), qlo - tr, qlo, itr, qv);
         Real f = -SM.lim_kup[lane] * up * (qv - qup) + SM.lim_klow[lane] * lo * (qlo - qv) - SM.lim_damp[lane] * (up + lo) * qd;
         Real diag = 0, tadd = f;
-        if (h > 0) {
-            Real dup = smooth_step_d(Real(0), Real(1), qup, qup + tr, itr, qv);
-            Real dlo = smooth_step_d(Real(1), Real(0), qlo - tr, qlo, itr, qv);
+        if (IMP_BF || (!IMP_BF && h > 0)) {   /* IMP_BF: no branch on h (at h = 0 this gives diag = 0, tadd = f) */
+            Real dup = smooth_step_d<BFK>(Real(0), Real(1), qup, qup + tr, itr, qv);
+            Real dlo = smooth_step_d<BFK>(Real(1), Real(0), qlo - tr, qlo, itr, qv);
             Real kq = SM.lim_kup[lane] * (up + dup * (qv - qup)) + SM.lim_klow[lane] * (lo - dlo * (qlo - qv));
             Real cq = SM.lim_damp[lane] * (up + lo);
             diag = h * cq + h * h * kq;
@@ -1672,17 +1834,29 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
 #pragma unroll
             for (int i = 0; i < 3; ++i) jd[i] += Sd[3 + i];
             PL::lin(jd);
-            const bool on = lds[LY::CW + 8 * sp + 6] > 0 && ((msk >> lane) & 1u);
-            r += on ? dot3m<ZV, 0>(jd, cj + 3) : Real(0);
-            if (implicit) {
+            /* weighted by on = 0 / 1 (every CJ value is finite: contact_compute
+             * is branch-free): a select made the compiler load cj under a
+             * branch, two basic blocks per sphere */
+            const bool onb = lds[LY::CW + 8 * sp + 6] > 0 && ((msk >> lane) & 1u);
+            const Real on = onb ? Real(1) : Real(0);
+            if constexpr (BFK) r = fma(on, dot3m<ZV, 0>(jd, cj + 3), r);
+            else r += onb ? dot3m<ZV, 0>(jd, cj + 3) : Real(0);
+            /* IMP (the semi-implicit kernels): no branch on h — a realize
+             * call (h = 0) has C = 0 (contact_compute), adding zeros */
+            if (IMP_BF || (!IMP_BF && implicit)) {
                 Real w[3] = {(ZV & 4u) ? C[0] * jd[0] : C[0] * jd[0] + C[1] * jd[2], C[2] * jd[1],
                              C[1] * jd[0] + C[3] * jd[2]};
                 Real pw[3];
                 cross3(cj, w, pw);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
-                    Gk[i] += on ? pw[i] : Real(0);
-                    Gk[3 + i] += on ? w[i] : Real(0);
+                    if constexpr (BFK) {
+                        Gk[i] = fma(on, pw[i], Gk[i]);
+                        Gk[3 + i] = fma(on, w[i], Gk[3 + i]);
+                    } else {
+                        Gk[i] += onb ? pw[i] : Real(0);
+                        Gk[3 + i] += onb ? w[i] : Real(0);
+                    }
                 }
             }
         });
@@ -1839,7 +2013,11 @@ template <class T, typename Real> struct IdArgs {
 };
 
 template <class T, typename Real>
+#ifndef BIOIM_ID_NO_WAVES_ATTR
 __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))) void id_kernel(IdArgs<T, Real> a) {
+#else   /* the compiler-crash reproducer (profiles/r03/regalloc_crash/): without the occupancy attribute */
+__global__ __launch_bounds__(BIOIM_WG) void id_kernel(IdArgs<T, Real> a) {
+#endif
     using LY = Lay<T, Real>;
     constexpr int G = T::G, ND = LY::ND, NB = T::NB, NP = LY::NP, EPB = BIOIM_WG / G;
     constexpr size_t SMB = smodel_bytes<T, Real>();
@@ -1876,7 +2054,7 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
     if constexpr (T::TX >= 0) {
         if constexpr (T::coord_dof[T::TX] >= 0) x0 = M.float_origin ? lds[LY::QF + T::TX] : Real(0);
     }
-    fn_slots<T, Real>(SM, lds, lane);
+    fn_slots<false, T, Real>(SM, lds, lane);
     if (lane < NB) kin_local<T, Real>(SM, lds, lane);
     if (lane == NB) kin_ground<T, Real>(lds, x0);
     wave_sync();
@@ -1920,14 +2098,14 @@ __global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))
         }
     }
     if (applied) {
-        if (lane < T::NS) contact_lane<T, Real>(SM, lds, lane, Real(0));
+        if (lane < T::NS) contact_lane<false, T, Real>(SM, lds, lane, Real(0));
         if (lane < T::NL) {
             const int cc = SM.lim_coord[lane];
             const Real qv = lds[LY::QF + cc], qdv = lds[LY::UF + cc];
             const Real qup = SM.lim_qup[lane], qlo = SM.lim_qlow[lane], tr = SM.lim_trans[lane];
             const Real itr = SM.lim_itrans[lane];
-            const Real up = smooth_step(Real(0), Real(1), qup, qup + tr, itr, qv);
-            const Real lo = smooth_step(Real(1), Real(0), qlo - tr, qlo, itr, qv);
+            const Real up = smooth_step<false>(Real(0), Real(1), qup, qup + tr, itr, qv);
+            const Real lo = smooth_step<false>(Real(1), Real(0), qlo - tr, qlo, itr, qv);
             lds[LY::LIM + 4 * lane] = -SM.lim_kup[lane] * up * (qv - qup) + SM.lim_klow[lane] * lo * (qlo - qv) -
                                       SM.lim_damp[lane] * (up + lo) * qdv;
         }
@@ -2511,7 +2689,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         const bool sub = remaining > 0;
         const bool eq = !sub && (pending_reset || eq_only);
         if (!sub && pending_reset) {
-            int r = clamp_row(reset_row, M.nrows);
+                        int r = clamp_row(reset_row, M.nrows);
             if (lane < ND) {
                 const int c = SM.dof_coord[lane];
                 qd = M.ref_q[r][c];
@@ -2552,7 +2730,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             /* RK: explicit accelerations (h = 0, the implicit terms compile away) */
             /* branch-free phase-3 row stores, except in the spatial RK kernels
              * (they would take those kernels past the 512-register budget) */
-            dynamics<T, Real, PERT, !RK || T::PLANAR>(*(const DModel<Real> *)Mi, SM, qd, ud, act, lce, control, lane, lds,
+            dynamics<T, Real, PERT, !RK || T::PLANAR, !RK>(*(const DModel<Real> *)Mi, SM, qd, ud, act, lce, control, lane, lds,
                                     RK ? Real(0) : (sub ? dt : Real(0)), eq && NM > 0, PA, pslot,
                                     RK ? 0 : M.nsub - remaining, D);
         }
@@ -2646,7 +2824,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             pending_reset = false;
             eq_only = false;
         }
-        /* ---- realized state: observation (lane-parallel; get_state_dict,
+                /* ---- realized state: observation (lane-parallel; get_state_dict,
          * muscle_walking_imitation_env2D.py:158-225).  The realize call left
          * the coordinates (QF/UF), frames (KB), contact wrenches (CW) and limit
          * forces (LIM) in LDS; report points first. */
@@ -2870,7 +3048,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[10] += __builtin_amdgcn_s_memtime() - k_t1;
 #endif
     /* ---- store state */
-    if (lane == 0) {
+        if (lane == 0) {
         st.t[env] = t;
         st.istep[env] = istep;
         st.has_last[env] = has_last;

@@ -12,10 +12,11 @@ for id in ${ids//,/ }; do
   for r in $(seq 1 "$rounds"); do
     for lib in "$@"; do
       tag=$(basename "$lib" .so)
+      [ "$tag" = libbioim ] && tag=$(basename "$(dirname "$lib")")   # build/ab/<variant>/libbioim.so
       if [ "$lib" = tree ]; then
-        timeout -k 10 120 python bench.py --no-cpu-baseline --env-id "$id" $BENCH_ARGS > "$out/${tag}__${id}__$r.json"
+        timeout -k 10 120 python bench.py --no-cpu-baseline --no-reference-integrator --no-single-env --env-id "$id" $BENCH_ARGS > "$out/${tag}__${id}__$r.json"
       else
-        BIOIM_LIB="$lib" timeout -k 10 120 python bench.py --no-cpu-baseline --env-id "$id" $BENCH_ARGS > "$out/${tag}__${id}__$r.json"
+        BIOIM_LIB="$lib" timeout -k 10 120 python bench.py --no-cpu-baseline --no-reference-integrator --no-single-env --env-id "$id" $BENCH_ARGS > "$out/${tag}__${id}__$r.json"
       fi
     done
   done

@@ -26,6 +26,13 @@ candidates, each classified:
   undefined   no earlier write and a read under wider EXEC: lanes outside
               the region read a register nothing wrote — the hazard.
 
+A candidate whose value reaches a memory instruction's address operand gets
+"+addr" (linear taint through VALU results); "masked-use+addr" and
+"undefined" are reported as risky: a lane that skipped the copy would load or
+store through a stale address — the fault incident class.  The fault of the
+r03i build (an RK kernel storing through an env offset copied to an AGPR
+only in the resume branch's lanes) scans as masked-use+addr.
+
     python tools/exec_hazard.py <file.s> [kernel-substring]
 """
 import re
@@ -99,6 +106,45 @@ def classify(ins, dep, i, start, dst, join_read):
     return 'masked-use' if dep[join_read] > 0 else 'undefined'
 
 
+MEM_ADDR_FIRST = ('global_store', 'flat_store', 'ds_write', 'scratch_store', 'buffer_store')
+MEM_ADDR_SECOND = ('global_load', 'flat_load', 'ds_read', 'scratch_load', 'buffer_load', 'global_atomic', 'ds_bpermute')
+
+
+def addr_operands(op, raw):
+    """the vector registers a memory instruction uses as its address"""
+    parts = raw.split(None, 1)
+    if len(parts) < 2:
+        return []
+    a = [x.strip() for x in parts[1].split(',')]
+    if op.startswith(MEM_ADDR_FIRST):
+        return regs(a[0]) if a else []
+    if op.startswith(MEM_ADDR_SECOND):
+        return regs(a[1]) if len(a) > 1 else []
+    return []
+
+
+def feeds_address(ins, j, reg, horizon=600):
+    """does the value read at j into `reg` (and anything computed from it)
+    reach a memory instruction's address operand before being overwritten?
+    Linear, conservative taint propagation through VALU results."""
+    taint = {reg} if isinstance(reg, str) else set(reg)
+    for k in range(j + 1, min(len(ins), j + horizon)):
+        op, dd, ss, raw = ins[k]
+        if any(r in taint for r in addr_operands(op, raw)):
+            return True
+        if op.startswith(('s_', 'global_store', 'ds_write', 'buffer_store', 'flat_store', 'scratch_store')):
+            continue
+        hit = any(r in taint for r in ss)
+        for d in dd:
+            if hit:
+                taint.add(d)
+            else:
+                taint.discard(d)
+        if not taint:
+            return False
+    return False
+
+
 def scan(ins):
     hits = []
     dep = depths(ins)
@@ -143,7 +189,14 @@ def scan(ins):
                 verdict = 'overwritten'
             j += 1
         if verdict == 'read-after-join':
-            hits.append((i, raw, j - 1, ins[j - 1][3], classify(ins, dep, i, start, dst, j - 1)))
+            kind = classify(ins, dep, i, start, dst, j - 1)
+            o, dd, ss, rr = ins[j - 1]
+            # the value read after the join reaches an address (a wrong lane value
+            # there is an out-of-range access: the fault incidents)
+            tainted = dd if o.startswith(('v_accvgpr_read', 'v_mov', 'v_accvgpr_write')) else [x for x in dst]
+            if feeds_address(ins, j - 1, tainted) or any(x in addr_operands(o, rr) for x in dst):
+                kind += '+addr'
+            hits.append((i, raw, j - 1, ins[j - 1][3], kind))
     return hits
 
 
@@ -159,8 +212,10 @@ def main():
         e = next(i for i in range(s, len(text)) if text[i].startswith('.Lfunc_end'))
         ins = parse(text[s:e])
         hits = scan(ins)
-        kinds = {k: sum(1 for h in hits if h[4] == k) for k in ('phi-merge', 'masked-use', 'undefined')}
-        print(f'{name[:90]}: {len(ins)} instructions, {len(hits)} candidate copies {kinds}')
+        kinds = {k: sum(1 for h in hits if h[4].split('+')[0] == k) for k in ('phi-merge', 'masked-use', 'undefined')}
+        risky = sum(1 for h in hits if h[4] in ('masked-use+addr', 'undefined', 'undefined+addr'))
+        print(f'{name[:90]}: {len(ins)} instructions, {len(hits)} candidate copies {kinds}, '
+              f'{risky} risky (masked-use into an address, or undefined)')
         for i, raw, j, use, kind in hits:
             print(f'    [{i}] {raw:50s} -> read after join at [{j}] {use:45s} {kind}')
 
