@@ -55,12 +55,6 @@ DEV void sfor(F &&f) {
 #ifndef BIOIM_ENV_MOD
 #define BIOIM_ENV_MOD -1
 #endif
-#ifndef BIOIM_BF_CURVE3D
-#define BIOIM_BF_CURVE3D 0
-#endif
-#ifndef BIOIM_BF_FV3D
-#define BIOIM_BF_FV3D 0
-#endif
 #ifndef BIOIM_BF_SPATIAL
 #define BIOIM_BF_SPATIAL 0
 #endif
@@ -1313,7 +1307,7 @@ template <typename Real> struct MState {
     bool clamped;
 };
 
-template <bool BFK, class T, typename Real>
+template <bool BFK, bool BFC, class T, typename Real>
 DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_state, Real l_state, Real excitation,
                      Real L, Real v_warm, MState<Real> &s) {
     STAMP_DECL
@@ -1336,16 +1330,16 @@ DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_
     const Real icos = lce * isq;          /* 1 / cos(pennation) */
     Real lt = L - sq;
     Real fse, dfse, fal, dfal, fpe, dfpe;
-    /* BF: the three curve chains and the fiber-velocity start in one basic
-     * block (planar kernels; the spatial fp64 kernels, two muscles per lane,
-     * would spill) */
-    curve_eval<BF || BIOIM_BF_CURVE3D>(Cfse, lt * mu.inv_lts, fse, dfse);
-    curve_eval<BF || BIOIM_BF_CURVE3D>(Cfal, lce * mu.inv_lopt, fal, dfal);
-    curve_eval<BF || BIOIM_BF_CURVE3D>(Cfpe, lce * mu.inv_lopt, fpe, dfpe);
+    /* BFC: the three curve chains and the fiber-velocity start and
+     * extrapolation in one basic block (every semi-implicit kernel; in the
+     * spatial ones only these, the other branch-free forms would spill) */
+    curve_eval<BFC>(Cfse, lt * mu.inv_lts, fse, dfse);
+    curve_eval<BFC>(Cfal, lce * mu.inv_lopt, fal, dfal);
+    curve_eval<BFC>(Cfpe, lce * mu.inv_lopt, fpe, dfpe);
     Real rhs = fse * icos - fpe;
     STAMP(16);
     Real vN, fvv, dfv;
-    solve_fv<BF || BIOIM_BF_FV3D>(Cfv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
+    solve_fv<BFC && (T::PLANAR || BIOIM_BF_SPATIAL)>(Cfv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
     STAMP(17);
     Real dGdv = a * fal * dfv + mu.beta;
     /* selects over plain locals (a load in a ?: arm or an if body becomes a
@@ -1633,6 +1627,10 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
      * lane-divergent copy of a live-in-all-lanes address into an AGPR and
      * faulted) */
     constexpr bool BFK = IMP_BF;
+    /* the muscle eval's curves and fiber-velocity solve in one block: every
+     * semi-implicit kernel (spatial too: no scratch, same-box 3D -3 %,
+     * profiles/r03/r03j/ab_branchfree_planar.txt, variant cf3d) */
+    constexpr bool BFC = IMP;
     STAMP_DECL
     publish_coords<T, Real>(M, SM, lds, lane, qd, ud);
     if (lane < ND) {
@@ -1743,7 +1741,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
                  * sphere lane holds a muscle): same block as the curve
                  * evaluations, so their chains interleave */
                 if constexpr (j == 0 && MUSCLE_CONTACT) contact_compute<BFK, T, Real>(SM, lds, lane < T::NS ? lane : 0, h, CO);
-                muscle_eval<BFK, T, Real>(SM, mu, a_, l_, control[j], L, D.ms[j].vN, D.ms[j]);
+                muscle_eval<BFK, BFC, T, Real>(SM, mu, a_, l_, control[j], L, D.ms[j].vN, D.ms[j]);
                 const Real nFt = -D.ms[j].Ft;
                 Real *ts = lds + LY::TAU + (lane + j * G) * T::MAXSPAN;
 #pragma unroll
@@ -2577,14 +2575,21 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             rk_hnext = 0;   /* reset_manager: a new Manager / integrator (opensim_wrapper.py:287-291) */
         }
     } else if (resume) {
-        /* the state is at the accepted RK point rk_t of the step ending at t */
+        /* the state is at the accepted RK point rk_t of the step ending at t.
+         * The loads index with an opaque copy of env made inside this
+         * lane-divergent branch: with env itself, the allocator split the
+         * kernel-long env offsets here and copied them into AGPRs for the
+         * resuming lanes only, which the state write-back then used as store
+         * addresses in every lane (the r03i fault) */
+        int er = env;
+        asm volatile("" : "+v"(er));
 #pragma unroll
         for (int j = 0; j < MPL; ++j) {
             const int m = mslot<T>(lane + j * G);
-            if (m < NA) { control[j] = st.ctl[(size_t)m * N + env]; curr[j] = st.cur[(size_t)m * N + env]; }
-            if (NM > 0 && m < NM) D.ms[j].vN = st.vnw[(size_t)m * N + env];
+            if (m < NA) { control[j] = st.ctl[(size_t)m * N + er]; curr[j] = st.cur[(size_t)m * N + er]; }
+            if (NM > 0 && m < NM) D.ms[j].vN = st.vnw[(size_t)m * N + er];
         }
-        rk_t = st.rkt[env]; rk_tf = t; rk_h = st.rkh[env]; rk_attempts = st.rka[env];
+        rk_t = st.rkt[er]; rk_tf = t; rk_h = st.rkh[er]; rk_attempts = st.rka[er];
         remaining = 1;
     } else if (mode == 0) {
         /* ---- action pre-processing (Env.step) */

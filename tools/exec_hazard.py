@@ -26,8 +26,11 @@ candidates, each classified:
   undefined   no earlier write and a read under wider EXEC: lanes outside
               the region read a register nothing wrote — the hazard.
 
-A candidate whose value reaches a memory instruction's address operand gets
-"+addr" (linear taint through VALU results); "masked-use+addr" and
+A candidate whose value reaches a memory instruction's address operand
+(linear taint through VALU results), copied at a deeper EXEC nesting than the
+read after the join (the nesting is tracked linearly: if/else pairs and loop
+exits make it approximate, so this prunes candidates heuristically), gets
+"+addr"; "masked-use+addr" and
 "undefined" are reported as risky: a lane that skipped the copy would load or
 store through a stale address — the fault incident class.  The fault of the
 r03i build (an RK kernel storing through an env offset copied to an AGPR
@@ -73,22 +76,36 @@ def is_join(op, raw):
     return op == 's_or_b64' and raw.split(None, 1)[1].startswith('exec, exec,')
 
 
+def writes_exec(op, raw):
+    parts = raw.split(None, 1)
+    return op.startswith('s_') and len(parts) > 1 and parts[1].startswith('exec,') and not is_join(op, raw)
+
+
 def depths(ins):
-    """EXEC nesting depth at each instruction (0: the kernel's full EXEC)"""
-    out, stack = [], []
+    """EXEC nesting depth at each instruction (0: the kernel's full EXEC).
+    A save by plain move (s_mov_b64 sX, exec: a loop, or an if whose
+    narrowing comes later) opens the region only at the instruction that
+    then narrows EXEC; until then the kernel still runs at the parent depth."""
+    out, stack, pending = [], [], None
     for op, dst, src, raw in ins:
         if op in ('s_and_saveexec_b64', 's_or_saveexec_b64', 's_andn2_saveexec_b64'):
             out.append(len(stack))
             stack.append(raw.split(None, 1)[1].split(',')[0].strip())
+            pending = None
             continue
         if op == 's_mov_b64' and raw.split(None, 1)[1].endswith(', exec'):
-            # EXEC saved by a plain move (a loop or an if/else whose then-part
-            # re-narrows with s_mov_b64 exec, ...): restored by s_or_b64 with it
+            pending = raw.split(None, 1)[1].split(',')[0].strip()
             out.append(len(stack))
-            stack.append(raw.split(None, 1)[1].split(',')[0].strip())
+            continue
+        if pending and writes_exec(op, raw):
+            out.append(len(stack))
+            stack.append(pending)
+            pending = None
             continue
         if is_join(op, raw):
             sv = raw.split(',')[-1].strip()
+            if sv == pending:
+                pending = None
             if sv in stack:        # a restore of a mask this scan did not see saved is not a join
                 while stack.pop() != sv:
                     pass
@@ -149,13 +166,23 @@ def scan(ins):
     hits = []
     dep = depths(ins)
     stack = []   # open regions: (saved-exec sgpr text, start index)
+    pending = None
     for i, (op, dst, src, raw) in enumerate(ins):
-        if op in ('s_and_saveexec_b64', 's_or_saveexec_b64', 's_andn2_saveexec_b64') or \
-                (op == 's_mov_b64' and raw.split(None, 1)[1].endswith(', exec')):
+        if op in ('s_and_saveexec_b64', 's_or_saveexec_b64', 's_andn2_saveexec_b64'):
             stack.append((raw.split(None, 1)[1].split(',')[0].strip(), i))
+            pending = None
+            continue
+        if op == 's_mov_b64' and raw.split(None, 1)[1].endswith(', exec'):
+            pending = raw.split(None, 1)[1].split(',')[0].strip()   # the region opens where EXEC narrows
+            continue
+        if pending and writes_exec(op, raw):
+            stack.append((pending, i))
+            pending = None
             continue
         if is_join(op, raw):
             sv = raw.split(',')[-1].strip()
+            if sv == pending:
+                pending = None
             if any(s == sv for s, _ in stack):
                 while stack.pop()[0] != sv:
                     pass
@@ -194,7 +221,11 @@ def scan(ins):
             # the value read after the join reaches an address (a wrong lane value
             # there is an out-of-range access: the fault incidents)
             tainted = dd if o.startswith(('v_accvgpr_read', 'v_mov', 'v_accvgpr_write')) else [x for x in dst]
-            if feeds_address(ins, j - 1, tainted) or any(x in addr_operands(o, rr) for x in dst):
+            # ... and the copy sits deeper in the EXEC nesting than that read: lanes
+            # active at the read were not all active at the copy (a copy at the read's
+            # own depth, e.g. after the kernel's early-return regions, covers them)
+            if (feeds_address(ins, j - 1, tainted) or any(x in addr_operands(o, rr) for x in dst)) \
+                    and dep[i] > dep[j - 1]:
                 kind += '+addr'
             hits.append((i, raw, j - 1, ins[j - 1][3], kind))
     return hits

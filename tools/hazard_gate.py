@@ -109,7 +109,7 @@ if __name__ == '__main__':
     if '--baseline' in sys.argv:   # record the per-kernel counts of a GPU-verified build
         import json
         out = os.path.join(os.path.dirname(HERE), 'profiles', 'r03', 'hazard_baseline.json')
-        json.dump({'build_dir': os.path.relpath(d, os.path.dirname(HERE)), 'risky': per_kernel(d)},
+        json.dump({'build': os.path.relpath(d, os.path.dirname(HERE)), 'risky': per_kernel(d)},
                   open(out, 'w'), indent=1, sort_keys=True)
         print('wrote', out)
         sys.exit(0)
