@@ -1339,7 +1339,7 @@ DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_
     Real rhs = fse * icos - fpe;
     STAMP(16);
     Real vN, fvv, dfv;
-    solve_fv<BFC && (T::PLANAR || BIOIM_BF_SPATIAL)>(Cfv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
+    solve_fv<BFC>(Cfv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
     STAMP(17);
     Real dGdv = a * fal * dfv + mu.beta;
     /* selects over plain locals (a load in a ?: arm or an if body becomes a
