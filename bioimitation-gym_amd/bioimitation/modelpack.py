@@ -412,6 +412,7 @@ def compile_pack(model: OsimModel, spec: EnvSpec, ref: dict) -> P.ModelPack:
             R, p = topo.body_X[sp.body]
             _set_vec(se.loc, R @ sp.loc + p)
             se.radius = sp.radius
+            se.obody = model.body_order.index(sp.body)
             sph_names[g] = ns
             ns += 1
     pk.nsphere = ns

@@ -78,7 +78,7 @@ class Muscle(C.Structure):
 
 
 class Sphere(C.Structure):
-    _fields_ = [('cbody', I), ('force', I), ('loc', D * 3), ('radius', D)]
+    _fields_ = [('cbody', I), ('force', I), ('loc', D * 3), ('radius', D), ('obody', I), ('pad_', I)]
 
 
 class CForce(C.Structure):

@@ -21,11 +21,13 @@ Manager's, the state after the reset and at every accepted Kutta-Merson step
   1), which would need a realize per accepted step.  With the fixed
   semi-implicit substeps the States storage too has one row per env step.
 - ForceReporter columns: each muscle / coordinate actuator (its actuation),
-  each Hunt-Crossley force's record values on the ground platform
-  (``<force>.ground.force.X..Z``, ``.torque.X..Z``: the six values the
-  reference itself reads and negates, opensim_wrapper.py:211-219), each
-  CoordinateLimitForce (its generalized force).  The contact record's
-  foot-side entries are not written (their layout is not pinned here).
+  each Hunt-Crossley force's record entries per geometry — the ground
+  platform's (``<force>.ground.force.X..Z``, ``.torque.X..Z``: the six values
+  the reference itself reads and negates, opensim_wrapper.py:211-219) and each
+  sphere's body (``<force>.<body>.force...``: the force's wrench on that body
+  about its origin, in ground, as HuntCrossleyForce::getRecordValues reports a
+  geometry's body force [upstream]) — and each CoordinateLimitForce (its
+  generalized force).
 
 Column names follow OpenSim 4.1:
 - states: ``/jointset/<joint>/<coord>/value``, ``/speed``,
@@ -139,9 +141,25 @@ class TrajectoryRecorder:
                                                                   [f'{c}_actuator' for c in self._act_coords()]))
             fr = np.array(self.force_rows)
             cols = [fr[:, :1 + pk.nact]]
+            # HuntCrossleyForce record (getRecordValues): per geometry in the
+            # force's order (platform first, then its spheres, opensim_utils.py:
+            # 14-81) the force and torque on that geometry's body, in ground:
+            # the platform's body is ground (the negated feet wrench), a
+            # sphere's entry is the whole force's wrench on the sphere's body
+            # about its origin, i.e. the sum over the force's spheres on it
+            bodies = list(self.names['bodies'])
+            so = 1 + pk.nact + 6 * pk.ncforce + pk.nlimit   # per-sphere foot-side values
+            sph = [(pk.sphere[s].force, pk.sphere[s].obody) for s in range(pk.nsphere)]
             for i, cf in enumerate(self.names['cforces']):
                 labels += [f'{cf}.ground.{k}.{x}' for k in ('force', 'torque') for x in 'XYZ']
                 cols.append(-fr[:, 1 + pk.nact + 6 * i:1 + pk.nact + 6 * i + 6])    # ground side = -(feet side)
+                if fr.shape[1] >= so + 6 * pk.nsphere:
+                    for s, (f, ob) in enumerate(sph):
+                        if f != i:
+                            continue
+                        labels += [f'{cf}.{bodies[ob]}.{k}.{x}' for k in ('force', 'torque') for x in 'XYZ']
+                        same = [s2 for s2, (f2, ob2) in enumerate(sph) if f2 == i and ob2 == ob]
+                        cols.append(sum(fr[:, so + 6 * s2:so + 6 * s2 + 6] for s2 in same))
             o = 1 + pk.nact + 6 * pk.ncforce
             labels += list(self.names['limits'])
             cols.append(fr[:, o:o + pk.nlimit])

@@ -1621,16 +1621,16 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
      * without a branch on h (the spatial kernels keep it: register budget) */
     constexpr bool IMP_BF = IMP && (T::PLANAR || BIOIM_BF_SPATIAL);
     /* the branch-free forms (selects over plain locals, blended
-     * extrapolations, one basic block per muscle eval) in the semi-implicit
-     * planar kernels only: the RK kernels keep the round-2 code, whose
-     * register allocation is GPU-verified (an RK build of these forms put a
-     * lane-divergent copy of a live-in-all-lanes address into an AGPR and
-     * faulted) */
-    constexpr bool BFK = IMP_BF;
-    /* the muscle eval's curves and fiber-velocity solve in one block: every
-     * semi-implicit kernel (spatial too: no scratch, same-box 3D -3 %,
-     * profiles/r03/r03j/ab_branchfree_planar.txt, variant cf3d) */
-    constexpr bool BFC = IMP;
+     * extrapolations, one basic block per muscle eval) in the planar
+     * kernels, except the torque-model RK ones: an RK build of these forms
+     * put a lane-divergent copy of a live-in-all-lanes address into an AGPR
+     * in the Torque2D RK kernel and faulted; that kernel
+     * keeps the GPU-verified code, and tools/hazard_gate.py checks the others */
+    constexpr bool BFK = (T::PLANAR || BIOIM_BF_SPATIAL) && (IMP || T::NM > 0);
+    /* the muscle eval's curves and fiber-velocity solve in one block, in
+     * every kernel (spatial too: no scratch; same-box 3D -1.6 %,
+     * profiles/r03/r03k, r03l) */
+    constexpr bool BFC = true;
     STAMP_DECL
     publish_coords<T, Real>(M, SM, lds, lane, qd, ud);
     if (lane < ND) {
@@ -2929,6 +2929,19 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                 for (int i = 0; i < 3; ++i) { fo[NA + 6 * lane + i] = F[i]; fo[NA + 6 * lane + 3 + i] = Mo[i]; }
             }
             if (lane < T::NL) fo[NA + 6 * T::NF + lane] = lds[LY::LIM + 4 * lane];
+            /* the contact record's foot-side entries: per sphere its force on
+             * its OpenSim body and the moment about that body's origin (the
+             * HuntCrossleyForce record sums these per body, in ground) */
+            if (lane < T::NS) {
+                const Real *cw = lds + LY::CW + 8 * lane;
+                const Real *rp = lds + LY::REP + 6 * SM.sph_ob[lane];   /* body origin, absolute x */
+                const Real O[3] = {rp[0] - x0, rp[1], rp[2]}, F[3] = {cw[0], cw[1], cw[2]};
+                Real oxf[3];
+                cross3(O, F, oxf);
+                Real *fs = fo + NA + 6 * T::NF + T::NL + 6 * lane;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) { fs[i] = F[i]; fs[3 + i] = cw[3 + i] - oxf[i]; }
+            }
         }
         if constexpr (REP) {
             if (osim && a.osim_out)
@@ -3361,7 +3374,7 @@ template <class T, typename Real> void build_smodel(const bioim_modelpack_t &p, 
     for (int s = 0; s < p.nsphere; ++s) {
         for (int i = 0; i < 3; ++i) m.sph_loc[s][i] = (Real)p.sphere[s].loc[i];
         m.sph_r[s] = (Real)p.sphere[s].radius;
-        m.sph_cb[s] = p.sphere[s].cbody; m.sph_force[s] = p.sphere[s].force;
+        m.sph_cb[s] = p.sphere[s].cbody; m.sph_force[s] = p.sphere[s].force; m.sph_ob[s] = p.sphere[s].obody;
     }
     for (int f = 0; f < p.ncforce; ++f) {
         const bioim_cforce_t &c = p.cforce[f];
@@ -3421,6 +3434,9 @@ template <class T> bool topology_matches(const bioim_modelpack_t &p) {
         p.n_obs_bpos != T::NOBP || p.n_obs_bvel != T::NOBV)
         return false;
     if (p.coord_tx != T::TX || p.coord_ty != T::TY || p.coord_tz != T::TZ) return false;
+    for (int s = 0; s < p.nsphere; ++s)   /* the report slot a sphere's foot-side record reads */
+        if (p.sphere[s].obody < 0 || p.sphere[s].obody >= p.nosbody || T::os_cb[p.sphere[s].obody] != p.sphere[s].cbody)
+            return false;
     if (p.npathpt != T::NPT || p.nfn != T::NFN || p.nknots != T::NKNOT) return false;
     {   /* moving-point function slots and muscle spans fit the compiled sizes */
         int nmf = 0;
@@ -3560,7 +3576,7 @@ LaunchArgs<T, Real> make_args(bioim_handle_t *h, int mode, const void *actions, 
     a.obs = reinterpret_cast<Real *>(obs);
     a.final_obs = mode == 0 ? reinterpret_cast<Real *>(h->final_obs) : nullptr;
     a.force_out = reinterpret_cast<Real *>(h->force_out);
-    a.force_dim = h->nact + 6 * h->pack.ncforce + h->pack.nlimit;   /* bioim_force_report_dim */
+    a.force_dim = h->nact + 6 * h->pack.ncforce + h->pack.nlimit + 6 * h->pack.nsphere;   /* bioim_force_report_dim */
     const bool integrates = mode == 0 || (oc && oc->op == BIOIM_OSIM_INTEGRATE);
     a.traj = integrates ? reinterpret_cast<Real *>(h->traj) : nullptr;
     a.traj_n = h->traj_n;
@@ -3944,7 +3960,7 @@ int bioim_pending_count(bioim_handle_t *h) {
 
 int bioim_force_report_dim(const bioim_handle_t *h) {
     if (!h) return fail(BIOIM_E_ARG, "null handle");
-    return h->nact + 6 * h->pack.ncforce + h->pack.nlimit;
+    return h->nact + 6 * h->pack.ncforce + h->pack.nlimit + 6 * h->pack.nsphere;
 }
 
 int bioim_set_state_storage(bioim_handle_t *h, void *rows, int capacity, int32_t *count) {

@@ -227,7 +227,10 @@ int bioim_set_final_obs(bioim_handle_t *h, void *final_obs);
  * [actuation of each muscle (tendon force, N) or coordinate actuator
  * (control x optimal force)] [per Hunt-Crossley force: force (3) and moment
  * about the ground origin (3) on the feet] [per CoordinateLimitForce: its
- * generalized force].  NULL disables it. */
+ * generalized force] [per contact sphere, pack order: its force (3) on its
+ * OpenSim body and the moment (3) about that body's origin, in ground — the
+ * HuntCrossleyForce record's foot-side entries sum these per body].  NULL
+ * disables it. */
 int bioim_force_report_dim(const bioim_handle_t *h);
 /* Optional state storage of the adaptive integrator (kind 1): OpenSim's
  * Manager stores the state at every accepted integration step, which

@@ -134,6 +134,8 @@ typedef struct {
     int32_t cbody, force;     /* composite body, owning HuntCrossleyForce        */
     double  loc[3];           /* center in composite frame                       */
     double  radius;
+    int32_t obody, pad_;      /* the OpenSim body (osbody index) the sphere is on:
+                                 its ForceReporter record entry (foot side)       */
 } bioim_sphere_t;
 
 typedef struct {

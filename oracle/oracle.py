@@ -124,7 +124,7 @@ class Oracle:
     def force_report(self, envs, i):
         """per-force-element values of env i's realized state (bioim_set_force_report layout)"""
         pk = self.pack
-        out = np.zeros(pk.nact + 6 * pk.ncforce + pk.nlimit)
+        out = np.zeros(pk.nact + 6 * pk.ncforce + pk.nlimit + 6 * pk.nsphere)
         self.lib.orc_force_report(self.pk, self.env_ptr(envs, i), _ptr(out))
         return out
 

@@ -140,19 +140,31 @@ def test_single_env_save_simulation_and_perturbation(tmp_path):
         states.append(orc.get_state(bufs, 0))
         forces.append(orc.force_report(bufs, 0))
     paths = env.osim_model.save_simulation(str(tmp_path))
-    # ForceReporter (opensim_wrapper.py:10-15, :338): actuators, ground-side contact records, limit forces
+    # ForceReporter (opensim_wrapper.py:10-15, :338): actuators, per contact force its record entries
+    # (the ground platform, then each sphere's body), limit forces
     hf, lf, df = read_sto(paths['forces'])
     fr = np.array(forces)
-    nf = pk.nact + 6 * pk.ncforce + pk.nlimit
-    assert df.shape == (7, 1 + nf) and lf[0] == 'time'
+    na, nf, nl, ns = pk.nact, pk.ncforce, pk.nlimit, pk.nsphere
+    assert df.shape == (7, 1 + na + 6 * nf + 6 * ns + nl) and lf[0] == 'time'
     names = load_names(env_id)
-    assert lf[1 + pk.nact:1 + pk.nact + 6] == [f'{names["cforces"][0]}.ground.{k}.{x}' for k in ('force', 'torque')
-                                                for x in 'XYZ']
-    np.testing.assert_allclose(df[:, 1:1 + pk.nact], fr[:, :pk.nact], rtol=1e-7, atol=1e-6)
-    np.testing.assert_allclose(df[:, 1 + pk.nact:1 + pk.nact + 6 * pk.ncforce], -fr[:, pk.nact:pk.nact + 6 * pk.ncforce],
-                               rtol=1e-6, atol=1e-4)
-    np.testing.assert_allclose(df[:, -pk.nlimit:], fr[:, -pk.nlimit:], rtol=1e-6, atol=1e-6)
-    assert np.abs(df[:, 1 + pk.nact:1 + pk.nact + 6 * pk.ncforce]).max() > 1.0     # feet on the ground
+    assert lf[1 + na:1 + na + 6] == [f'{names["cforces"][0]}.ground.{k}.{x}' for k in ('force', 'torque')
+                                     for x in 'XYZ']
+    sph = [(pk.sphere[s].force, pk.sphere[s].obody) for s in range(ns)]
+    assert lf[1 + na + 6:1 + na + 12] == [f'{names["cforces"][0]}.{names["bodies"][sph[0][1]]}.{k}.{x}'
+                                          for k in ('force', 'torque') for x in 'XYZ']
+    so = na + 6 * nf + nl
+    want = []
+    for f in range(nf):
+        want.append(-fr[:, na + 6 * f:na + 6 * f + 6])
+        for s, (ff, ob) in enumerate(sph):
+            if ff == f:
+                want.append(sum(fr[:, so + 6 * s2:so + 6 * s2 + 6] for s2, (f2, o2) in enumerate(sph)
+                                if f2 == f and o2 == ob))
+    np.testing.assert_allclose(df[:, 1:1 + na], fr[:, :na], rtol=1e-7, atol=1e-6)
+    np.testing.assert_allclose(df[:, 1 + na:1 + na + 6 * nf + 6 * ns], np.hstack(want), rtol=1e-6, atol=1e-4)
+    np.testing.assert_allclose(df[:, -nl:], fr[:, na + 6 * nf:na + 6 * nf + nl], rtol=1e-6, atol=1e-6)
+    ground = np.hstack([want[k] for k in range(len(want)) if k % (1 + ns // nf) == 0])   # the platform entries
+    assert np.abs(ground).max() > 1.0                        # feet on the ground
     h, labels, data = read_sto(paths['states'])
     assert data.shape[0] == 7
     np.testing.assert_allclose(data[:, 0], [s[0] for s in states], atol=1e-9)

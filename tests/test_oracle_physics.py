@@ -195,3 +195,41 @@ def test_energy_conserved_without_dissipation(oracle_lib, env_id):
     for _ in range(5):
         o.step(envs, 0, np.full(pk.nact, np.nan))   # NaN -> zero torques
     assert abs(energy() - e0) < 2e-3 * (abs(e0) + 1)
+
+
+@pytest.mark.parametrize('env_id', ['MuscleWalkingImitation2D-v0', 'MuscleRunningImitation3D-v0'])
+def test_contact_record_foot_side_entries(oracle_lib, env_id):
+    """The ForceReporter's Hunt-Crossley entries per sphere body (the force's
+    wrench on the sphere's OpenSim body about its origin, force report tail):
+    per contact force they sum, with each body origin's moment arm, to the
+    force's wrench on the feet about the ground origin (the negated platform
+    entry) — the third law the record's two sides must satisfy."""
+    from bioimitation.simulation_io import split_osim_report
+    pk = load_pack(env_id)
+    orc = oracle_lib.Oracle(pk)
+    bufs = orc.new_envs(1)
+    orc.reset(bufs, 0, 0)
+    st = orc.get_state(bufs, 0)
+    dy = pk.coord[pk.coord_ty].dof
+    st[5 + dy] -= 0.02                                   # 2 cm into the ground
+    orc.set_state(bufs, 0, st)
+    fr = orc.force_report(bufs, 0)
+    rep = split_osim_report(pk, orc.osim_report(bufs, 0))
+    na, nf, nl = pk.nact, pk.ncforce, pk.nlimit
+    so = na + 6 * nf + nl
+    assert len(fr) == so + 6 * pk.nsphere
+    loaded = 0
+    for f in range(nf):
+        F = np.zeros(3)
+        M = np.zeros(3)
+        for s in range(pk.nsphere):
+            if pk.sphere[s].force != f:
+                continue
+            Fs, Ts = fr[so + 6 * s:so + 6 * s + 3], fr[so + 6 * s + 3:so + 6 * s + 6]
+            O = rep['bodies'][pk.sphere[s].obody][:3]
+            F += Fs
+            M += Ts + np.cross(O, Fs)
+        np.testing.assert_allclose(F, fr[na + 6 * f:na + 6 * f + 3], rtol=1e-12, atol=1e-9)
+        loaded += np.linalg.norm(F) > 10.0
+        np.testing.assert_allclose(M, fr[na + 6 * f + 3:na + 6 * f + 6], rtol=1e-10, atol=1e-8)
+    assert loaded >= 1                                   # a foot on the ground

@@ -140,14 +140,16 @@ def addr_operands(op, raw):
     return []
 
 
-def feeds_address(ins, j, reg, horizon=600):
+def feeds_address(ins, j, reg, horizon=600, lds=False):
     """does the value read at j into `reg` (and anything computed from it)
-    reach a memory instruction's address operand before being overwritten?
-    Linear, conservative taint propagation through VALU results."""
+    reach the address operand of a global / flat / scratch / buffer access
+    (lds=True: of an LDS access) before being overwritten?  Linear,
+    conservative taint propagation through VALU results.  A wrong lane value
+    in a global address is a memory fault; in an LDS address a wrong value."""
     taint = {reg} if isinstance(reg, str) else set(reg)
     for k in range(j + 1, min(len(ins), j + horizon)):
         op, dd, ss, raw = ins[k]
-        if any(r in taint for r in addr_operands(op, raw)):
+        if op.startswith('ds_') == lds and any(r in taint for r in addr_operands(op, raw)):
             return True
         if op.startswith(('s_', 'global_store', 'ds_write', 'buffer_store', 'flat_store', 'scratch_store')):
             continue
@@ -224,9 +226,12 @@ def scan(ins):
             # ... and the copy sits deeper in the EXEC nesting than that read: lanes
             # active at the read were not all active at the copy (a copy at the read's
             # own depth, e.g. after the kernel's early-return regions, covers them)
-            if (feeds_address(ins, j - 1, tainted) or any(x in addr_operands(o, rr) for x in dst)) \
-                    and dep[i] > dep[j - 1]:
-                kind += '+addr'
+            direct = any(x in addr_operands(o, rr) for x in dst)
+            if dep[i] > dep[j - 1]:
+                if feeds_address(ins, j - 1, tainted) or (direct and not o.startswith('ds_')):
+                    kind += '+addr'
+                elif feeds_address(ins, j - 1, tainted, lds=True) or direct:
+                    kind += '+ldsaddr'
             hits.append((i, raw, j - 1, ins[j - 1][3], kind))
     return hits
 
