@@ -188,11 +188,15 @@ struct SModel {
     int32_t rw_slot[BIOIM_NREFBODY];     /* report slots of the reward's reference bodies  */
     /* root-to-body joint chain, front-padded with the identity joint slot NB */
     int32_t chain[T::NB][TopoInfo<T>::depth()];
-    int32_t sph_cb[D::NSD], sph_force[D::NSD], sph_ob[D::NSD], lim_coord[D::NLD], lim_dof[D::NLD], act_dof[D::NAD];
+    int32_t sph_cb[D::NSD], sph_force[D::NSD], lim_coord[D::NLD], lim_dof[D::NLD], act_dof[D::NAD];
     /* muscle torque gather (lane = dof): the TAU slots (muscle slot s, span
      * entry k -> s * MAXSPAN + k) holding -F_t dL/dq_d, padded with the zero
      * slot */
     uint8_t tau_src[D::NDD][T::MAXARM];
+    /* force-report body of each contact sphere (its OpenSim body, a report
+     * slot); last and byte-sized so that it lands in the image's 16-byte
+     * round-up and leaves every other offset where it was */
+    uint8_t sph_ob[D::NSD];
 };
 
 /* bytes of the LDS image (16-byte granules for the cooperative copy) */
