@@ -55,6 +55,9 @@ DEV void sfor(F &&f) {
 #ifndef BIOIM_ENV_MOD
 #define BIOIM_ENV_MOD -1
 #endif
+#ifndef BIOIM_BF3
+#define BIOIM_BF3 26
+#endif
 #ifndef BIOIM_BF_SPATIAL
 #define BIOIM_BF_SPATIAL 0
 #endif
@@ -1619,7 +1622,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     static_assert(NB < G && ND <= G, "lane NB writes the ground slot; one lane per dof");
     /* the semi-implicit planar kernels: the implicit contact / limit terms
      * without a branch on h (the spatial kernels keep it: register budget) */
-    constexpr bool IMP_BF = IMP && (T::PLANAR || BIOIM_BF_SPATIAL);
+    constexpr bool IMP_BF = IMP && (T::PLANAR || BIOIM_BF_SPATIAL || ((BIOIM_BF3 & 64) && !PERT));
     /* the branch-free forms (selects over plain locals, blended
      * extrapolations, one basic block per muscle eval) in the planar
      * kernels, except the torque-model RK ones: an RK build of these forms
@@ -1627,6 +1630,15 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
      * in the Torque2D RK kernel and faulted; that kernel
      * keeps the GPU-verified code, and tools/hazard_gate.py checks the others */
     constexpr bool BFK = (T::PLANAR || BIOIM_BF_SPATIAL) && (IMP || T::NM > 0);
+    /* per-piece switches of the branch-free forms in the spatial semi-implicit
+     * kernels (BIOIM_BF3 bits: 1 function slots, 2 muscle paths, 4 contact,
+     * 8 limits, 16 fiber equilibrium, 32 phase-3 rows, 64 implicit
+     * terms without a branch on h, 128 muscle eval) */
+    constexpr bool BF3 = !T::PLANAR && IMP;
+    constexpr bool BFK_FN = BFK || (BF3 && (BIOIM_BF3 & 1)), BFK_PATH = BFK || (BF3 && (BIOIM_BF3 & 2));
+    constexpr bool BFK_CON = BFK || (BF3 && (BIOIM_BF3 & 4)), BFK_LIM = BFK || (BF3 && (BIOIM_BF3 & 8));
+    constexpr bool BFK_EQ = BFK || (BF3 && (BIOIM_BF3 & 16)), BFK_ROW = BFK || (BF3 && (BIOIM_BF3 & 32));
+    constexpr bool BFK_ME = BFK || (BF3 && (BIOIM_BF3 & 128));
     /* the muscle eval's curves and fiber-velocity solve in one block, in
      * every kernel (spatial too: no scratch; same-box 3D -1.6 %,
      * profiles/r03/r03k, r03l) */
@@ -1647,7 +1659,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     /* ---- phase 0b: function slots, one lane each — the moving path points'
      * location functions (read by every muscle that has the point) and the
      * joints' spline axes (read by their body's lane) */
-    fn_slots<BFK, T, Real>(SM, lds, lane);
+    fn_slots<BFK_FN, T, Real>(SM, lds, lane);
     STAMP(15);
 
     /* ---- phase 1: lane-parallel kinematics */
@@ -1729,19 +1741,19 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
             if (m < T::NM) {
                 const SMuscle<Real> &mu = SM.mus[m];
                 Real L, dLs[T::MAXSPAN];
-                muscle_path<BFK, T, Real>(SM, mu, lds, L, dLs);
+                muscle_path<BFK_PATH, T, Real>(SM, mu, lds, L, dLs);
                 STAMP(4);
                 Real a_ = act[j], l_ = lce[j];
                 if (equilibrate) /* equilibrateMuscles: static fiber equilibrium at the held activation
                                   * (a reset has set the default activation) */
-                    l_ = muscle_equilibrium<BFK, T, Real>(SM, mu, a_, L);
+                    l_ = muscle_equilibrium<BFK_EQ, T, Real>(SM, mu, a_, L);
                 D.act[j] = a_;
                 D.lce[j] = l_;
                 /* the sphere contacts ride in the first muscle pass (every
                  * sphere lane holds a muscle): same block as the curve
                  * evaluations, so their chains interleave */
-                if constexpr (j == 0 && MUSCLE_CONTACT) contact_compute<BFK, T, Real>(SM, lds, lane < T::NS ? lane : 0, h, CO);
-                muscle_eval<BFK, BFC, T, Real>(SM, mu, a_, l_, control[j], L, D.ms[j].vN, D.ms[j]);
+                if constexpr (j == 0 && MUSCLE_CONTACT) contact_compute<BFK_CON, T, Real>(SM, lds, lane < T::NS ? lane : 0, h, CO);
+                muscle_eval<BFK_ME, BFC, T, Real>(SM, mu, a_, l_, control[j], L, D.ms[j].vN, D.ms[j]);
                 const Real nFt = -D.ms[j].Ft;
                 Real *ts = lds + LY::TAU + (lane + j * G) * T::MAXSPAN;
 #pragma unroll
@@ -1761,20 +1773,20 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     if constexpr (MUSCLE_CONTACT) {
         if (lane < T::NS) contact_store<T, Real>(lds, lane, CO);
     } else {
-        if (lane < T::NS) contact_lane<BFK, T, Real>(SM, lds, lane, h);
+        if (lane < T::NS) contact_lane<BFK_CON, T, Real>(SM, lds, lane, h);
     }
     STAMP(6);
     if (lane < T::NL) {
         int cc = SM.lim_coord[lane];
         Real qv = lds[LY::QF + cc], qd = lds[LY::UF + cc];
         Real qup = SM.lim_qup[lane], qlo = SM.lim_qlow[lane], tr = SM.lim_trans[lane], itr = SM.lim_itrans[lane];
-        Real up = smooth_step<BFK>(Real(0), Real(1), qup, qup + tr, itr, qv);
-        Real lo = smooth_step<BFK>(Real(1), Real(0), qlo - tr, qlo, itr, qv);
+        Real up = smooth_step<BFK_LIM>(Real(0), Real(1), qup, qup + tr, itr, qv);
+        Real lo = smooth_step<BFK_LIM>(Real(1), Real(0), qlo - tr, qlo, itr, qv);
         Real f = -SM.lim_kup[lane] * up * (qv - qup) + SM.lim_klow[lane] * lo * (qlo - qv) - SM.lim_damp[lane] * (up + lo) * qd;
         Real diag = 0, tadd = f;
         if (IMP_BF || (!IMP_BF && h > 0)) {   /* IMP_BF: no branch on h (at h = 0 this gives diag = 0, tadd = f) */
-            Real dup = smooth_step_d<BFK>(Real(0), Real(1), qup, qup + tr, itr, qv);
-            Real dlo = smooth_step_d<BFK>(Real(1), Real(0), qlo - tr, qlo, itr, qv);
+            Real dup = smooth_step_d<BFK_LIM>(Real(0), Real(1), qup, qup + tr, itr, qv);
+            Real dlo = smooth_step_d<BFK_LIM>(Real(1), Real(0), qlo - tr, qlo, itr, qv);
             Real kq = SM.lim_kup[lane] * (up + dup * (qv - qup)) + SM.lim_klow[lane] * (lo - dlo * (qlo - qv));
             Real cq = SM.lim_damp[lane] * (up + lo);
             diag = h * cq + h * h * kq;
@@ -1837,7 +1849,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
              * branch, two basic blocks per sphere */
             const bool onb = lds[LY::CW + 8 * sp + 6] > 0 && ((msk >> lane) & 1u);
             const Real on = onb ? Real(1) : Real(0);
-            if constexpr (BFK) r = fma(on, dot3m<ZV, 0>(jd, cj + 3), r);
+            if constexpr (BFK_ROW) r = fma(on, dot3m<ZV, 0>(jd, cj + 3), r);
             else r += onb ? dot3m<ZV, 0>(jd, cj + 3) : Real(0);
             /* IMP (the semi-implicit kernels): no branch on h — a realize
              * call (h = 0) has C = 0 (contact_compute), adding zeros */
@@ -1848,7 +1860,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
                 cross3(cj, w, pw);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
-                    if constexpr (BFK) {
+                    if constexpr (BFK_ROW) {
                         Gk[i] = fma(on, pw[i], Gk[i]);
                         Gk[3 + i] = fma(on, w[i], Gk[3 + i]);
                     } else {
