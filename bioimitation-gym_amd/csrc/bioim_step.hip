@@ -56,7 +56,7 @@ DEV void sfor(F &&f) {
 #define BIOIM_ENV_MOD -1
 #endif
 #ifndef BIOIM_BF3
-#define BIOIM_BF3 26
+#define BIOIM_BF3 122
 #endif
 #ifndef BIOIM_BF_SPATIAL
 #define BIOIM_BF_SPATIAL 0

@@ -1,7 +1,8 @@
-# evidence pass on the tree build (spatial branch-free pieces BIOIM_BF3=26):
-# GPU tests, smoke, bench lines, rocprof passes; then same-box A/B of further
-# BIOIM_BF3 variants against it
+# final check of the tree build (BIOIM_BF3=122): GPU tests, smoke, C4 and C3 bench lines
 set -o pipefail
-mkdir -p gpurun_out/r03s
-bash tools/gpu_r03.sh r03s && \
-bash tools/ab.sh gpurun_out/r03s/ab3 3 MuscleRunningImitation3D-v0 bioimitation-gym_amd/build/ab/bf58/libbioim.so bioimitation-gym_amd/build/ab/bf122/libbioim.so tree > gpurun_out/r03s/ab3.log 2>&1
+O=gpurun_out/r03u
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 && \
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 && \
+timeout -k 10 200 python bench.py --env-id MuscleRunningImitation3D-v0 --no-cpu-baseline --no-single-env > $O/bench_3d.json 2> $O/bench.err && \
+timeout -k 10 200 python bench.py --no-cpu-baseline --no-single-env --no-reference-integrator > $O/bench_2d.json 2>> $O/bench.err
