@@ -19,6 +19,7 @@ reference tables and to cross-check the compiled topology in tests.
 from __future__ import annotations
 
 import ctypes
+import struct
 import math
 from dataclasses import dataclass
 from typing import Dict, List, Optional
@@ -508,9 +509,16 @@ def pack_bytes(pk: P.ModelPack) -> bytes:
 
 
 def pack_from_bytes(b: bytes) -> P.ModelPack:
+    # the header (magic, version) first: an outdated pack is refused by its
+    # version, not by a size mismatch of a layout it does not have
+    if len(b) < 8:
+        raise ValueError(f'pack of {len(b)} bytes has no header')
+    magic, version = struct.unpack_from('<II', b, 0)
+    if magic != P.MAGIC:
+        raise ValueError(f'bad ModelPack magic {magic:#x}')
+    if version != P.VERSION:
+        raise ValueError(f'ModelPack version {version}, this build reads version {P.VERSION}: rebuild the pack '
+                         '(bioimitation-gym_amd/tools/build_packs.py)')
     if len(b) != ctypes.sizeof(P.ModelPack):
         raise ValueError(f'pack size {len(b)} != {ctypes.sizeof(P.ModelPack)}')
-    pk = P.ModelPack.from_buffer_copy(b)
-    if pk.magic != P.MAGIC or pk.version != P.VERSION:
-        raise ValueError('bad ModelPack magic/version')
-    return pk
+    return P.ModelPack.from_buffer_copy(b)

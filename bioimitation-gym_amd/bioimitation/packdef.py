@@ -3,7 +3,7 @@ tests/test_modelpack.py checks sizeof against both shared libraries)."""
 import ctypes as C
 
 MAGIC = 0x4D4F4942
-VERSION = 2
+VERSION = 3   # include/bioim_modelpack.h BIOIM_PACK_VERSION
 
 MAX_COORD = 24
 MAX_CBODY = 12

@@ -40,6 +40,8 @@ from __future__ import annotations
 import math
 import os
 
+import warnings
+
 import numpy as np
 
 from .storage import write_sto
@@ -407,24 +409,32 @@ class OsimModelFacade:
         self._record()
 
     def storage(self):
-        """the last env step's accepted integration steps (RK; None otherwise)"""
+        """the last env step's accepted integration steps (RK; None otherwise).
+        A step with more accepted steps than the buffer holds keeps its first
+        ``cap`` rows and warns: the recording is optional, the step itself is
+        complete (the reference just integrates)."""
         env = self._env
         if getattr(env, 'storage_rows', None) is None:
             return None
         k = int(env.storage_count[self._i])
         cap = env.storage_rows.shape[1]
         if k > cap:
-            raise RuntimeError(f'state storage overflow: {k} accepted steps, capacity {cap}')
+            warnings.warn(f'state storage: {k} accepted integration steps in one env step, the buffer holds '
+                          f'{cap}; the rows after the first {cap} are not recorded', RuntimeWarning)
+            k = cap
         return env.storage_rows[self._i, :k].double().cpu().numpy()
 
     def _record(self, stepped=True):
-        r = self._rep
-        self.recorder.record(self._state()[self._i], r['qdd'], self._force_row(r),
+        """one analysis row: the state, q'' of the realize and the ForceReporter
+        row (``bioim_set_force_report``, the same full row ImitationEnv records:
+        actuations, feet wrenches, limits and the per-sphere body entries)"""
+        env = self._env
+        if getattr(env, 'force_report', None) is None:
+            env.enable_force_report()
+            self._call('realize')          # fills the force row of the current state
+        r = self.report()
+        self.recorder.record(self._state()[self._i], r['qdd'], env.force_report[self._i].double().cpu().numpy(),
                              storage=self.storage() if stepped else None)
-
-    @staticmethod
-    def _force_row(r):
-        return np.concatenate([r['actuation'], r['contact'].reshape(-1), r['limits']])
 
     # ------------------------------------------------------------ realizations
     def calc_joint_kinematics(self):

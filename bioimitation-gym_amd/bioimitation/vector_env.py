@@ -204,9 +204,7 @@ class VectorEnv:
         if getattr(self, 'osim_report', None) is None:
             d = _lib.check(self._L.bioim_osim_report_dim(self._h))
             self.osim_report = torch.zeros((self.num_envs, d), dtype=self.dtype, device=self.device)
-        ids = torch.as_tensor(env_ids, dtype=torch.int32, device=self.device).reshape(-1).contiguous()
-        if ids.numel() and (int(ids.min()) < 0 or int(ids.max()) >= self.num_envs):
-            raise ValueError(f'env ids must lie in [0, {self.num_envs})')
+        ids = self._env_ids(env_ids)
         ctl = None
         if controls is not None:
             ctl = torch.as_tensor(controls, dtype=self.dtype, device=self.device).reshape(ids.numel(), self.action_dim)
@@ -215,6 +213,20 @@ class VectorEnv:
         _lib.check(self._L.bioim_osim(self._h, OSIM_OPS[op], self._ptr(ids), ids.numel(), self._ptr(ctl),
                                       self._ptr(self.obs) if want_obs else None, self._ptr(self.osim_report)))
         return self.osim_report
+
+    def _env_ids(self, env_ids):
+        """validated int32 device tensor of env ids: in range (a stray id is an
+        out-of-bounds store in the kernel) and distinct (two lane groups would
+        race on one env's state)"""
+        import torch
+        ids = torch.as_tensor(env_ids, dtype=torch.int32, device=self.device).reshape(-1).contiguous()
+        if ids.numel():
+            h = ids.cpu()
+            if int(h.min()) < 0 or int(h.max()) >= self.num_envs:
+                raise ValueError(f'env ids must lie in [0, {self.num_envs})')
+            if h.unique().numel() != h.numel():
+                raise ValueError('env ids must be distinct')
+        return ids
 
     def pending_count(self) -> int:
         """Envs suspended mid-step by the RK budget."""
@@ -234,7 +246,7 @@ class VectorEnv:
         ids = rows = None
         n = self.num_envs
         if env_ids is not None:
-            ids = torch.as_tensor(env_ids, dtype=torch.int32, device=self.device).contiguous()
+            ids = self._env_ids(env_ids)
             n = ids.numel()
         if ref_index is not None:
             rows = torch.as_tensor(ref_index, dtype=torch.int32, device=self.device).contiguous()

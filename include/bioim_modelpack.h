@@ -24,7 +24,7 @@
 #include <stdint.h>
 
 #define BIOIM_PACK_MAGIC   0x4D4F4942u /* "BIOM" */
-#define BIOIM_PACK_VERSION 2
+#define BIOIM_PACK_VERSION 3 /* 3: bioim_sphere_t carries obody (40 -> 48 bytes) */
 
 #define BIOIM_MAX_COORD    24
 #define BIOIM_MAX_CBODY    12

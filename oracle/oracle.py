@@ -44,6 +44,7 @@ class Oracle:
             ('orc_mass_matrix_bias', None, [C.c_void_p, _dp, _dp, _dp, _dp]),
             ('orc_forward_dynamics', C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
             ('orc_muscle_path', None, [C.c_void_p, _dp, _dp, C.c_int, _dp, _dp, _dp]),
+            ('orc_muscle_paths', None, [C.c_void_p, _dp, _dp, _dp, _dp, _dp]),
             ('orc_curve', C.c_double, [C.c_void_p, C.c_int, C.c_int, C.c_double, _dp]),
             ('orc_fn', C.c_double, [C.c_void_p, C.c_int, C.c_double, _dp, _dp]),
             ('orc_muscle_equilibrium', C.c_double, [C.c_void_p, C.c_int, C.c_double, C.c_double]),
@@ -241,6 +242,15 @@ class Oracle:
         u = np.ascontiguousarray(u, dtype=np.float64)
         self.lib.orc_muscle_path(self.pk, _ptr(q), _ptr(u), int(m), C.byref(L), C.byref(Ld), _ptr(d))
         return L.value, Ld.value, d
+
+    def muscle_paths(self, q, u):
+        """(L[nm], dL/dt[nm], dL/dq[nm][nd]) of every muscle from one kinematics pass"""
+        nm, nd = self.pack.nmuscle, self.pack.ndof
+        L, Ld, d = np.zeros(nm), np.zeros(nm), np.zeros((nm, nd))
+        q = np.ascontiguousarray(q, dtype=np.float64)
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        self.lib.orc_muscle_paths(self.pk, _ptr(q), _ptr(u), _ptr(L), _ptr(Ld), _ptr(d))
+        return L, Ld, d
 
     def curve(self, m, which, x):
         d = C.c_double()

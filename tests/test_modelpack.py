@@ -149,3 +149,18 @@ def test_committed_packs_are_current():
         fresh = modelpack.pack_bytes(modelpack.compile_pack(model, registry.env_spec(env_id), ref))
         committed = modelpack.pack_bytes(load_pack(env_id))
         assert fresh == committed, env_id
+
+
+def test_outdated_pack_version_is_refused():
+    """A pack of another layout version is refused by its header (magic,
+    version) before its size is looked at: BIOIM_PACK_VERSION 3 added the
+    sphere's OpenSim body (bioim_sphere_t 40 -> 48 bytes)."""
+    import struct
+    from bioimitation.modelpack import pack_bytes, pack_from_bytes
+    from bioimitation.registry import load_pack
+    b = bytearray(pack_bytes(load_pack('MuscleWalkingImitation2D-v0')))
+    assert struct.unpack_from('<II', b, 0) == (0x4D4F4942, 3)
+    struct.pack_into('<I', b, 4, 2)
+    for blob in (bytes(b), bytes(b[:-8 * 8])):       # same size, and a smaller (older) layout
+        with pytest.raises(ValueError, match='version 2'):
+            pack_from_bytes(blob)

@@ -28,7 +28,14 @@ class OracleVectorEnv:
         self.num_envs = n
         self.integrator_accuracy = 1e-3
         self.obs = torch.zeros((n, self.pack.obs_dim), dtype=torch.float64)
+        self.force_report = None
         self.calls = []
+
+    def enable_force_report(self, on=True):
+        import torch
+        pk = self.pack
+        self.force_report = torch.zeros((self.num_envs, pk.nact + 6 * pk.ncforce + pk.nlimit + 6 * pk.nsphere),
+                                        dtype=torch.float64) if on else None
 
     def get_state(self):
         return np.stack([self.orc.get_state(self.bufs, i) for i in range(self.num_envs)])
@@ -48,6 +55,8 @@ class OracleVectorEnv:
             elif op == 'integrate':
                 self.orc.osim_integrate(self.bufs, i)
             rep[i] = self.orc.osim_report(self.bufs, i)
+            if self.force_report is not None:
+                self.force_report[i] = torch.as_tensor(self.orc.force_report(self.bufs, i))
             if want_obs:
                 self.obs[i] = torch.as_tensor(self.orc.observe(self.bufs, i))
         self.calls.append(op)
@@ -202,3 +211,27 @@ def test_multibody_order_restatement():
     order = om.get_coordinate_names_multibody_order()
     assert order[:6] == ['pelvis_tilt', 'pelvis_list', 'hip_adduction_r', 'hip_rotation_r', 'pelvis_ty', 'pelvis_tz']
     assert len(order) == 14 and set(order) < set(om.coordinate_names)
+
+
+def test_facade_records_the_full_force_report_row(tmp_path):
+    """The facade records the same ForceReporter row the env's step records
+    (bioim_set_force_report: actuations, feet wrenches, limits and the
+    per-sphere body entries), so a run that mixes facade calls and env steps
+    (the reference's tests/example_position_control.py) writes one table with
+    the per-body ``<force>.<body>.*`` columns."""
+    from bioimitation.storage import read_sto
+    venv, om = _facade('MuscleWalkingImitation2D-v0')
+    pk = venv.pack
+    om.reset()
+    om.set_time(pk.ref_time[30])
+    om.set_coordinates({n: pk.ref_q[30][c] for c, n in enumerate(om.coordinate_names)})
+    om.actuate(np.full(pk.nact, 0.3))
+    om.integrate()
+    om.integrate()
+    width = pk.nact + 6 * pk.ncforce + pk.nlimit + 6 * pk.nsphere
+    assert {len(r) for r in om.recorder.force_rows} == {1 + width}
+    np.testing.assert_array_equal(om.recorder.force_rows[-1][1:], venv.orc.force_report(venv.bufs, 0))
+    paths = om.save_simulation(str(tmp_path))
+    h, labels, data = read_sto(paths['forces'])
+    assert data.shape[0] == len(om.recorder.force_rows) and np.isfinite(data).all()
+    assert any('.calcn_r.force.X' in l for l in labels), labels

@@ -7,12 +7,11 @@ read uses as a memory address ("masked-use+addr") or that no lane wrote
 5.5: the r03i build faulted in such a kernel.
 
     python tools/hazard_gate.py [build-dir] [-v]     # list risky copies; exit 1 if any
-    python tools/hazard_gate.py [build-dir] --baseline   # record a GPU-verified build's counts
+    python tools/hazard_gate.py [build-dir] --baseline   # record the per-kernel counts (profiles/r04)
 
 The scan is conservative (it cannot tell that a later region selects a subset
-of the copy's lanes), so GPU-verified kernels carry some candidates;
-tests/test_hazard_gate.py fails when a kernel has more than in the recorded
-GPU-verified build (profiles/r03/hazard_baseline.json).
+of the copy's lanes); the shipped build carries none in any of its 126
+kernels, and tests/test_hazard_gate.py requires exactly that.
 """
 from __future__ import annotations
 
@@ -108,7 +107,7 @@ if __name__ == '__main__':
     d = args[0] if args else os.path.join(os.path.dirname(HERE), 'bioimitation-gym_amd', 'build')
     if '--baseline' in sys.argv:   # record the per-kernel counts of a GPU-verified build
         import json
-        out = os.path.join(os.path.dirname(HERE), 'profiles', 'r03', 'hazard_baseline.json')
+        out = os.path.join(os.path.dirname(HERE), 'profiles', 'r04', 'hazard_baseline.json')
         json.dump({'build': os.path.relpath(d, os.path.dirname(HERE)), 'risky': per_kernel(d)},
                   open(out, 'w'), indent=1, sort_keys=True)
         print('wrote', out)
