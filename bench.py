@@ -155,14 +155,21 @@ def single_env_rate(env_id='TorqueWalkingImitation2D-v0', steps=300):
     return out
 
 
-def _profile_record(name, key):
+def _profile_record(name, key, build_id):
+    """profiles/<name>[key] (rocprofv3 evidence, tools/ingest_evidence.py) with
+    ``stale`` set when the record was taken on another build than the library
+    this bench loaded (its ``build_id`` differs from bioim_build_id())"""
     path = os.path.join(REPO, 'profiles', name)
     if not os.path.exists(path):
         return None
     try:
-        return json.load(open(path)).get(key)
+        rec = json.load(open(path)).get(key)
     except (OSError, ValueError):
         return None
+    if rec is not None:
+        rec = dict(rec)
+        rec['stale'] = rec.get('build_id') != build_id
+    return rec
 
 
 def _spawn_ranks(a):
@@ -308,20 +315,24 @@ def main():
             B = algorithmic_bytes_per_env_step(env.pack, real_bytes)
         achieved = B * n / (kernel_ms * 1e-3) / 1e9
         key = f'{a.env_id}/fp{a.precision}/{n}'
-        tr = _profile_record('traffic.json', key)
-        traffic = tr['bytes'] if tr else None          # rocprofv3 2 x FETCH_SIZE + WRITE_SIZE per launch
+        build_id = env.build_id
+        tr = _profile_record('traffic.json', key, build_id)
+        # rocprofv3 2 x FETCH_SIZE + WRITE_SIZE per launch, only when measured on this very build
+        traffic = tr['bytes'] if tr and not tr['stale'] else None
         roofline = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                     'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                     'traffic_over_algorithmic': traffic / (B * n) if traffic else None,
                     'bytes_per_env_step': B, 'kernel_ms': kernel_ms}
         if tr:
             roofline['traffic_source'] = tr.get('source')
+            roofline['traffic_build_id'] = tr.get('build_id')
+            roofline['traffic_stale'] = tr['stale']
         line = {
             'metric': 'env steps/sec (whole node), MuscleWalkingImitation2D-v0 @ 4096 envs/GPU'
             if a.env_id == 'MuscleWalkingImitation2D-v0' and n == 4096 else f'env steps/sec, {a.env_id} @ {n} envs/GPU',
             'value': value, 'unit': 'env-steps/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
             'burn_in': a.burn_in, 'ms_per_step': t_max / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': f'f{a.precision}', 'done_rate': done_rate,
+            'vs_baseline': None, 'dtype': f'f{a.precision}', 'done_rate': done_rate, 'build_id': build_id,
             'data': 'synthetic: PCG64 U[0,1] muscle excitations; reference motion synthesized from the shipped 3D IK',
             'config': {'workload': f'{a.env_id} batched env.step, {n} envs/GPU, ' +
                        (f'nsub={env.nsub}' if a.integrator == 'semi-implicit' else 'RK-Merson 1e-3') + ', auto-reset',
@@ -330,7 +341,7 @@ def main():
                        'launch': env.launch},
             'roofline': roofline,
         }
-        valu = _profile_record('valu.json', key)
+        valu = _profile_record('valu.json', key, build_id)
         if valu:   # the bound that is live for this kernel, from the rocprofv3 SQ passes
             line['valu'] = valu
         if a.rk_budget:

@@ -228,6 +228,11 @@ class VectorEnv:
                 raise ValueError('env ids must be distinct')
         return ids
 
+    @property
+    def build_id(self) -> str:
+        """bioim_build_id() of the loaded library (sources + flags hash)"""
+        return self._L.bioim_build_id().decode()
+
     def pending_count(self) -> int:
         """Envs suspended mid-step by the RK budget."""
         return _lib.check(self._L.bioim_pending_count(self._h))
@@ -349,6 +354,10 @@ class MixedVectorEnv:
             off += e.num_envs
         self._hs = (C.c_void_p * len(self.envs))(*[e._h.value for e in self.envs])
         self._L = self.envs[0]._L
+
+    @property
+    def build_id(self) -> str:
+        return self._L.bioim_build_id().decode()
 
     def reset(self):
         for e in self.envs:

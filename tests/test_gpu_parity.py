@@ -688,12 +688,15 @@ def test_parity_200_steps_muscle_tracking_drive(env_id):
     from the oracle's state and go to the GPU, the oracle and an ensemble of
     four one-ulp oracle twins.
 
-    Bounds, on every env alive on all sides at every step: obs and reward
-    within 1e-4 relative (north_star) while the twin envelope stays within
-    1e-5, and within max(1e-7, 100 x the twin envelope) throughout; `done`
-    equal; >= 50 % of the envs alive at t = 200 on the oracle and on the GPU
-    (the episode limit istep >= N ends rows drawn near reset_hi before t = 200:
-    those count as not alive)."""
+    Bounds per env and step, while the env is alive on all sides: obs and
+    reward within 1e-4 relative (north_star) whenever that env's twin
+    envelope is within 1e-5 (most env-steps: the drive is not chaotic; an
+    env whose twins diverge — a rounding-level perturbation grown by contact
+    events — is held to the next bound only), and within
+    max(1e-7, 100 x its twin envelope) at every step; `done` equal; >= 50 %
+    of the envs alive at t = 200 on the oracle and on the GPU (the episode
+    limit istep >= N ends rows drawn near reset_hi before t = 200: those
+    count as not alive)."""
     import torch
     from tracking import TrackingDrive, load_schedule, make_twin, twin_columns
     from bioimitation.obslayout import load_names
@@ -711,7 +714,8 @@ def test_parity_200_steps_muscle_tracking_drive(env_id):
             make_twin(orc, tw, i, c)
     live = np.ones(n, bool)                      # alive on the GPU, the oracle and every twin
     orc_alive, gpu_alive = np.ones(n, bool), np.ones(n, bool)
-    e_gpu, e_twin = np.zeros(T), np.zeros(T)
+    e_gpu, e_twin = np.zeros((T, n)), np.zeros((T, n))
+    seen = np.zeros((T, n), bool)
     for t in range(T):
         acts = np.stack([drive(orc.get_state(bufs, i), sched[i, t // P]) for i in range(n)])
         obs, rew, done = (v.cpu().numpy() for v in env.step(torch.as_tensor(acts, device=env.device))[:3])
@@ -720,23 +724,28 @@ def test_parity_200_steps_muscle_tracking_drive(env_id):
             dt = False
             for tw in twins:
                 o2, r2, d2, _ = orc.step(tw, i, acts[i])
-                if live[i]:
-                    e_twin[t] = max(e_twin[t], _rel(o2, o).max(), abs(r2 - r) / max(1.0, abs(r)))
+                e_twin[t, i] = max(e_twin[t, i], _rel(o2, o).max(), abs(r2 - r) / max(1.0, abs(r)))
                 dt = dt or d2
             if live[i]:
-                e_gpu[t] = max(e_gpu[t], _rel(obs[i], o).max(), abs(rew[i] - r) / max(1.0, abs(r)))
+                seen[t, i] = True
+                e_gpu[t, i] = max(_rel(obs[i], o).max(), abs(rew[i] - r) / max(1.0, abs(r)))
                 assert bool(done[i]) == d, (t, i)
             orc_alive[i] &= not d
             gpu_alive[i] &= not bool(done[i])
             live[i] = live[i] and not (d or dt or done[i])
+    calm = seen & (e_twin <= 1e-5)
+    eg, et = np.where(seen, e_gpu, 0).max(1), np.where(seen, e_twin, 0).max(1)
     ks = [0, 49, 99, 149, 199]
-    calm = e_twin <= 1e-5
-    print(f'{env_id} 200 steps, scheduled tracking drive, rows {list(rows)}: alive at t=200 oracle '
-          f'{orc_alive.sum()}/{n}, GPU {gpu_alive.sum()}/{n}; max rel err GPU vs oracle / oracle vs its one-ulp '
-          f'twins at t=' + ', '.join(f'{k + 1}: {e_gpu[k]:.1e} / {e_twin[k]:.1e}' for k in ks) +
-          f'; twin <= 1e-5 for {calm.sum()}/{T} steps; GPU max {e_gpu.max():.1e}; '
-          f'worst GPU/twin ratio {np.max(e_gpu / np.maximum(1e-30, e_twin)):.1f}')
-    assert (e_gpu[calm] < 1e-4).all(), (np.where(calm & (e_gpu >= 1e-4))[0], e_gpu.max())
-    assert (e_gpu <= np.maximum(1e-7, 100 * e_twin)).all(), int(np.argmax(e_gpu / np.maximum(1e-30, e_twin)))
+    ratio = np.where(seen, e_gpu / np.maximum(1e-30, e_twin), 0)
+    print(f'{env_id} 200 steps, scheduled tracking drive, rows {[int(r) for r in rows]}: alive at t=200 oracle '
+          f'{orc_alive.sum()}/{n}, GPU {gpu_alive.sum()}/{n}; max over envs of the rel err GPU vs oracle / '
+          f'oracle vs its one-ulp twins at t=' + ', '.join(f'{k + 1}: {eg[k]:.1e} / {et[k]:.1e}' for k in ks) +
+          f'; calm env-steps (twin <= 1e-5) {calm.sum()}/{seen.sum()}, GPU max there {e_gpu[calm].max():.1e}; '
+          f'per-env worst twin {" ".join(f"{x:.0e}" for x in np.where(seen, e_twin, 0).max(0))}; '
+          f'worst GPU/twin ratio {ratio.max():.1f}')
+    assert (e_gpu[calm] < 1e-4).all(), np.argwhere(calm & (e_gpu >= 1e-4))[:5]
+    bad = seen & (e_gpu > np.maximum(1e-7, 100 * e_twin))
+    assert not bad.any(), np.argwhere(bad)[:5]
+    assert calm.sum() >= 0.9 * seen.sum(), (calm.sum(), seen.sum())
     assert orc_alive.sum() >= n // 2 and gpu_alive.sum() >= n // 2, (orc_alive.sum(), gpu_alive.sum())
     env.close()

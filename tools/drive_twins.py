@@ -34,6 +34,7 @@ def run(env_id, T=200, ntwins=4):
             make_twin(orc, tw, i, c)
     live, alive = np.ones(n, bool), np.ones(n, bool)
     e_twin = np.zeros(T)
+    e_env = np.zeros((T, n))
     for t in range(T):
         for i in range(n):
             a = drive(orc.get_state(bufs, i), sched[i, t // P])
@@ -42,18 +43,22 @@ def run(env_id, T=200, ntwins=4):
             for tw in twins:
                 o2, r2, d2, _ = orc.step(tw, i, a)
                 if live[i]:
-                    e_twin[t] = max(e_twin[t], (np.abs(o2 - o) / np.maximum(1.0, np.abs(o))).max(),
-                                    abs(r2 - r) / max(1.0, abs(r)))
+                    e = max((np.abs(o2 - o) / np.maximum(1.0, np.abs(o))).max(), abs(r2 - r) / max(1.0, abs(r)))
+                    e_twin[t] = max(e_twin[t], e)
+                    e_env[t, i] = max(e_env[t, i], e)
                 dt = dt or d2
             alive[i] &= not d
             live[i] = live[i] and not (d or dt)
-    return rows, alive, e_twin
+    return rows, alive, e_twin, e_env
 
 
 if __name__ == '__main__':
     env_id = sys.argv[1]
-    rows, alive, e = run(env_id)
+    rows, alive, e, ee = run(env_id)
     print(f'{env_id}: rows {list(rows)}; alive at t=200 {alive.sum()}/{len(rows)}')
     print('twin envelope at t=1,25,50,75,100,125,150,175,200:',
           ' '.join(f'{e[k]:.1e}' for k in (0, 24, 49, 74, 99, 124, 149, 174, 199)))
     print(f'steps with twin <= 1e-5: {(e <= 1e-5).sum()}/200; first above: {int(np.argmax(e > 1e-5)) if (e > 1e-5).any() else None}')
+    calm = ee <= 1e-5
+    print('per env: worst twin', ' '.join(f'{x:.0e}' for x in ee.max(0)))
+    print(f'env-steps with the env\'s twin <= 1e-5: {calm.sum()}/{calm.size}')
