@@ -44,6 +44,31 @@
 /* env flags baked into a kernel (topologies.h FLAGS); RAW_ACTION, TARGET_OBS, GRF_OBS are run-time */
 #define BIOIM_STRUCT_FLAGS (BIOIM_ENV_MUSCLE | BIOIM_ENV_HAS_TZ | BIOIM_ENV_REWARD_FEET | BIOIM_ENV_DONE_CROSS | BIOIM_ENV_PD)
 
+#ifndef BIOIM_CHECK
+#define BIOIM_CHECK 0
+#endif
+/* BIOIM_CHECK=1 (a diagnostic build, never shipped): every global load and
+ * store of the env kernel goes through a bounds check that prints the source
+ * line, the index, the bound, the workgroup and the thread, then traps — the
+ * stale-lane class of DESIGN.md 5.5 then ends as a named trap instead of an
+ * anonymous illegal-address fault.  With BIOIM_CHECK=0 the accessors expand to
+ * plain subscripts (the shipped kernels are unchanged). */
+DEV size_t bioim_chk(size_t i, size_t n, int line) {
+    if (i >= n) {
+        printf("BIOIM_CHECK bioim_step.hip:%d index %llu outside [0, %llu) workgroup %u thread %u\n", line,
+               (unsigned long long)i, (unsigned long long)n, blockIdx.x, threadIdx.x);
+        __builtin_trap();
+    }
+    return i;
+}
+#if BIOIM_CHECK
+#define GAT(p, i, n) ((p)[bioim_chk((size_t)(i), (size_t)(n), __LINE__)])
+#define GIDX(i, n) bioim_chk((size_t)(i), (size_t)(n), __LINE__)
+#else
+#define GAT(p, i, n) ((p)[i])
+#define GIDX(i, n) (i)
+#endif
+
 template <int I, int N, class F>
 DEV void sfor(F &&f) {
     if constexpr (I < N) {
@@ -1602,7 +1627,7 @@ DEV Real pert_force(const PertArgs<Real> &P, double *sl, int k) {
         }
         sl[2] = lo >= 0 ? P.x[lo] : -INFINITY;
         sl[3] = hi < P.n ? P.x[hi] : INFINITY;
-        sl[4] = (double)P.y[(size_t)(lo >= 0 ? lo : 0) * P.N + P.env];
+        sl[4] = (double)GAT(P.y, (size_t)(lo >= 0 ? lo : 0) * P.N + P.env, (size_t)P.n * P.N);
     }
     return (Real)sl[4];
 }
@@ -2050,9 +2075,9 @@ __global__ __launch_bounds__(BIOIM_WG) void id_kernel(IdArgs<T, Real> a) {
     const bool need_m = op == BIOIM_ID_MULT_M || op == BIOIM_ID_MULT_MINV || op == BIOIM_ID_RESIDUAL;
     Real qd = 0, ud = 0, vd = 0;
     if (lane < ND) {
-        qd = a.q[(size_t)idx * ND + lane];
-        ud = use_u ? a.u[(size_t)idx * ND + lane] : Real(0);
-        vd = (need_m || op == BIOIM_ID_MULT_MINV) ? a.v[(size_t)idx * ND + lane] : Real(0);
+        qd = GAT(a.q, (size_t)idx * ND + lane, (size_t)a.n * ND);
+        ud = use_u ? GAT(a.u, (size_t)idx * ND + lane, (size_t)a.n * ND) : Real(0);
+        vd = (need_m || op == BIOIM_ID_MULT_MINV) ? GAT(a.v, (size_t)idx * ND + lane, (size_t)a.n * ND) : Real(0);
     }
     publish_coords<T, Real>(M, SM, lds, lane, qd, ud);
     if (lane < ND) {
@@ -2194,7 +2219,7 @@ __global__ __launch_bounds__(BIOIM_WG) void id_kernel(IdArgs<T, Real> a) {
         else if (op == BIOIM_ID_RESIDUAL) r = mv + bias - fa;
         else r = bias - fa;
     }
-    if (lane < ND) a.out[(size_t)idx * ND + lane] = r;
+    if (lane < ND) GAT(a.out, (size_t)idx * ND + lane, (size_t)a.n * ND) = r;
 }
 
 /* ---------------------------------------------------------------- kernel
@@ -2470,12 +2495,12 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     int env;
     if (mode == 1 || osim) {
         if (gidx >= a.n_list) return;
-        env = a.env_ids ? a.env_ids[gidx] : gidx;
+        env = a.env_ids ? GAT(a.env_ids, gidx, a.n_list) : gidx;
         if (env < 0 || env >= N) return;
     } else {
         if (gidx >= N) return;
         env = gidx;
-        if (a.active && !a.active[env] && !(RK && st.pend[env] != 0)) return;
+        if (a.active && !GAT(a.active, env, N) && !(RK && GAT(st.pend, env, (size_t)N) != 0)) return;
     }
     const int H = M.horizon;
     constexpr int MPL = LY::MPL;                  /* muscles / actions per lane: m = lane + j*G */
@@ -2485,25 +2510,25 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     for (int j = 0; j < MPL; ++j) D.ms[j].vN = 0;
     /* lane d < ND owns dof d (coordinate value qd, speed ud) */
     Real qd = 0, ud = 0;
-    if (lane < ND) { qd = st.q[(size_t)lane * N + env]; ud = st.u[(size_t)lane * N + env]; }
-    double t = st.t[env];
-    int istep = st.istep[env], has_last = st.has_last[env], resets = st.resets[env];
-    Real old_px = st.old_px[env];
+    if (lane < ND) { qd = GAT(st.q, (size_t)lane * N + env, (size_t)ND * N); ud = GAT(st.u, (size_t)lane * N + env, (size_t)ND * N); }
+    double t = GAT(st.t, env, (size_t)N);
+    int istep = GAT(st.istep, env, (size_t)N), has_last = GAT(st.has_last, env, (size_t)N), resets = GAT(st.resets, env, (size_t)N);
+    Real old_px = GAT(st.old_px, env, (size_t)N);
     Real act[MPL], lce[MPL], control[MPL], curr[MPL], last[MPL], hist[MPL][BIOIM_MAX_HORIZON];
 #pragma unroll
     for (int j = 0; j < MPL; ++j) {
         const int m = mslot<T>(lane + j * G);
         act[j] = 0; lce[j] = 0; control[j] = 0; curr[j] = 0; last[j] = 0;
-        if (NM > 0 && m < NM) { act[j] = st.act[(size_t)m * N + env]; lce[j] = st.lce[(size_t)m * N + env]; }
+        if (NM > 0 && m < NM) { act[j] = GAT(st.act, (size_t)m * N + env, (size_t)(NM > 0 ? NM : 1) * N); lce[j] = GAT(st.lce, (size_t)m * N + env, (size_t)(NM > 0 ? NM : 1) * N); }
 #pragma unroll
         for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh) hist[j][hh] = 0;
         if (m < NA) {
-            last[j] = st.last[(size_t)m * N + env];
+            last[j] = GAT(st.last, (size_t)m * N + env, (size_t)NA * N);
 #pragma unroll
             for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
-                hist[j][hh] = hh < H ? st.hist[((size_t)hh * NA + m) * N + env] : Real(0);
+                hist[j][hh] = hh < H ? GAT(st.hist, ((size_t)hh * NA + m) * N + env, (size_t)BIOIM_MAX_HORIZON * NA * N) : Real(0);
             /* held controls (OsimModel calls act on the last actuate) */
-            if (osim) control[j] = st.ctl[(size_t)m * N + env];
+            if (osim) control[j] = GAT(st.ctl, (size_t)m * N + env, (size_t)NA * N);
         }
     }
     int done = 0;
@@ -2511,7 +2536,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     bool do_reset = (mode == 1);
     /* budgeted RK: a suspended step resumes (its action row is ignored) */
     const bool budget = RK && a.rk_budget > 0;
-    const bool resume = RK && mode == 0 && st.pend[env] != 0;
+    const bool resume = RK && mode == 0 && GAT(st.pend, env, (size_t)N) != 0;
     bool suspend = false;
     /* RK: dynamics evaluations spent in this launch (the budget is 5 per
      * attempt) and so far (bioim_eval_count).  (Reusing a rejected attempt's
@@ -2521,14 +2546,14 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
      * launch from a step; profiles/r03/ab_dropped/ab_rk_k1_reuse.txt) */
     int launch_evals = 0;
     /* state-storage rows of this env step so far (a resumed step continues its count) */
-    int traj_k = (RK && a.traj && mode == 0 && st.pend[env] != 0) ? a.traj_n[env] : 0;
+    int traj_k = (RK && a.traj && mode == 0 && GAT(st.pend, env, (size_t)N) != 0) ? GAT(a.traj_n, env, N) : 0;
     int reset_row = 0;
-    if (mode == 1) reset_row = a.ref_index ? a.ref_index[gidx] : draw_index(a.seed, a.env_offset + env, resets, M.reset_hi);
+    if (mode == 1) reset_row = a.ref_index ? GAT(a.ref_index, gidx, a.n_list) : draw_index(a.seed, a.env_offset + env, resets, M.reset_hi);
 
     int remaining = 0;
     Real dt = 0;
     /* RK kernels: current step [rk_t, rk_t + rk_h], stage, attempts, next step size */
-    double rk_t = 0, rk_tf = 0, rk_h = 0, rk_hnext = RK ? st.hrk[env] : 0.0;
+    double rk_t = 0, rk_tf = 0, rk_h = 0, rk_hnext = RK ? GAT(st.hrk, env, (size_t)N) : 0.0;
     int rk_stage = 0, rk_attempts = 0;
     bool rk_last = false, rk_fail = false;
     Real y0q = 0, y0u = 0, Kq = 0, Ku = 0, Eq = 0, Eu = 0, rk_err = 0;
@@ -2567,7 +2592,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
 #pragma unroll
             for (int j = 0; j < MPL; ++j) {
                 const int m = mslot<T>(lane + j * G);
-                raw[j] = m < NA ? a.controls_in[(size_t)gidx * NA + m] : Real(0);
+                raw[j] = m < NA ? GAT(a.controls_in, (size_t)gidx * NA + m, (size_t)a.n_list * NA) : Real(0);
                 nan_here = nan_here || (m < NA && isnan(raw[j]));
             }
             const bool anynan = group_any<G>(nan_here);
@@ -2578,7 +2603,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                 const Real hi = NM > 0 ? Real(1) : SM.ca_max[ms];
                 const Real v = anynan ? Real(0) : raw[j];
                 control[j] = m < NA ? (v < lo ? lo : (v > hi ? hi : v)) : Real(0);
-                if (m < NA) st.ctl[(size_t)m * N + env] = control[j];
+                if (m < NA) GAT(st.ctl, (size_t)m * N + env, (size_t)NA * N) = control[j];
             }
         }
         if (a.osim_op == BIOIM_OSIM_INTEGRATE) begin_integrate();
@@ -2598,10 +2623,10 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
 #pragma unroll
         for (int j = 0; j < MPL; ++j) {
             const int m = mslot<T>(lane + j * G);
-            if (m < NA) { control[j] = st.ctl[(size_t)m * N + er]; curr[j] = st.cur[(size_t)m * N + er]; }
-            if (NM > 0 && m < NM) D.ms[j].vN = st.vnw[(size_t)m * N + er];
+            if (m < NA) { control[j] = GAT(st.ctl, (size_t)m * N + er, (size_t)NA * N); curr[j] = GAT(st.cur, (size_t)m * N + er, (size_t)NA * N); }
+            if (NM > 0 && m < NM) D.ms[j].vN = GAT(st.vnw, (size_t)m * N + er, (size_t)(NM > 0 ? NM : 1) * N);
         }
-        rk_t = st.rkt[er]; rk_tf = t; rk_h = st.rkh[er]; rk_attempts = st.rka[er];
+        rk_t = GAT(st.rkt, er, (size_t)N); rk_tf = t; rk_h = GAT(st.rkh, er, (size_t)N); rk_attempts = GAT(st.rka, er, (size_t)N);
         remaining = 1;
     } else if (mode == 0) {
         /* ---- action pre-processing (Env.step) */
@@ -2610,7 +2635,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
 #pragma unroll
         for (int j = 0; j < MPL; ++j) {
             const int m = mslot<T>(lane + j * G);
-            raw[j] = m < NA ? actions[(size_t)env * a.act_stride + m] : Real(0);
+            raw[j] = m < NA ? GAT(actions, (size_t)env * a.act_stride + m, (size_t)N * a.act_stride) : Real(0);
             nan_here = nan_here || (m < NA && isnan(raw[j]));
         }
         const bool anynan = group_any<G>(nan_here);
@@ -2660,7 +2685,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             if (m < NA) {
 #pragma unroll
                 for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
-                    if (hh < H) st.hist[((size_t)hh * NA + m) * N + env] = hist[j][hh];
+                    if (hh < H) GAT(st.hist, ((size_t)hh * NA + m) * N + env, (size_t)BIOIM_MAX_HORIZON * NA * N) = hist[j][hh];
             }
             const Real phys = (M.env_flags & BIOIM_ENV_RAW_ACTION) ? av[j] : curr[j];
             pnan_here = pnan_here || (m < NA && isnan(phys));
@@ -2678,7 +2703,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             /* the held controls (PrescribedController's Constants): kept through
              * resets, read by resets and OsimModel calls; stored now, so they
              * are not held in registers past the last dynamics call */
-            if (m < NA) st.ctl[(size_t)m * N + env] = control[j];
+            if (m < NA) GAT(st.ctl, (size_t)m * N + env, (size_t)NA * N) = control[j];
         }
         /* ---- integrate to step_size * istep */
         begin_integrate();
@@ -2725,7 +2750,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
 #pragma unroll
             for (int j = 0; j < MPL; ++j) {
                 const int m = mslot<T>(lane + j * G);
-                control[j] = m < NA ? st.ctl[(size_t)m * N + env] : Real(0);
+                control[j] = m < NA ? GAT(st.ctl, (size_t)m * N + env, (size_t)NA * N) : Real(0);
                 if constexpr (NM > 0)
                     if (m < NM) act[j] = SM.mus[m].default_act;
             }
@@ -2792,14 +2817,14 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                 if (!rk_last) rk_hnext = rk_h * fac;
                 if (a.traj) {   /* the Manager stores every accepted step (opensim_wrapper.py:336) */
                     if (traj_k < a.traj_cap) {
-                        Real *row = a.traj + ((size_t)env * a.traj_cap + traj_k) * a.traj_dim;
-                        if (lane == 0) row[0] = Real(rk_t);
-                        if (lane < ND) { row[1 + lane] = qd; row[1 + ND + lane] = ud; }
+                        Real *row = a.traj + GIDX(((size_t)env * a.traj_cap + traj_k), (size_t)N * a.traj_cap) * a.traj_dim;
+                        if (lane == 0) GAT(row, 0, a.traj_dim) = Real(rk_t);
+                        if (lane < ND) { GAT(row, 1 + lane, a.traj_dim) = qd; GAT(row, 1 + ND + lane, a.traj_dim) = ud; }
                         if constexpr (NM > 0) {
 #pragma unroll
                             for (int j = 0; j < MPL; ++j) {
                                 const int m = mslot<T>(lane + j * G);
-                                if (m < NM) { row[1 + 2 * ND + m] = act[j]; row[1 + 2 * ND + NM + m] = lce[j]; }
+                                if (m < NM) { GAT(row, 1 + 2 * ND + m, a.traj_dim) = act[j]; GAT(row, 1 + 2 * ND + NM + m, a.traj_dim) = lce[j]; }
                             }
                         }
                     }
@@ -2917,13 +2942,13 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             /* ForceReporter values (opensim_wrapper.py:10-15): actuation of each
              * muscle (tendon force) or coordinate actuator, the wrench on the feet
              * of each contact force about the ground origin, each limit force */
-            Real *fo = a.force_out + (size_t)env * a.force_dim;
+            Real *fo = a.force_out + GIDX((size_t)env, (size_t)N) * a.force_dim;
 #pragma unroll
             for (int j = 0; j < MPL; ++j) {
                 const int m = mslot<T>(lane + j * G);
                 if (m < NA) {
-                    if constexpr (NM > 0) fo[m] = D.ms[j].Ft;
-                    else fo[m] = control[j] * SM.ca_opt[m];
+                    if constexpr (NM > 0) GAT(fo, m, a.force_dim) = D.ms[j].Ft;
+                    else GAT(fo, m, a.force_dim) = control[j] * SM.ca_opt[m];
                 }
             }
             if (lane < T::NF) {
@@ -2938,9 +2963,9 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                 Mo[1] += -x0 * F[2];
                 Mo[2] += x0 * F[1];
 #pragma unroll
-                for (int i = 0; i < 3; ++i) { fo[NA + 6 * lane + i] = F[i]; fo[NA + 6 * lane + 3 + i] = Mo[i]; }
+                for (int i = 0; i < 3; ++i) { GAT(fo, NA + 6 * lane + i, a.force_dim) = F[i]; GAT(fo, NA + 6 * lane + 3 + i, a.force_dim) = Mo[i]; }
             }
-            if (lane < T::NL) fo[NA + 6 * T::NF + lane] = lds[LY::LIM + 4 * lane];
+            if (lane < T::NL) GAT(fo, NA + 6 * T::NF + lane, a.force_dim) = lds[LY::LIM + 4 * lane];
             /* the contact record's foot-side entries: per sphere its force on
              * its OpenSim body and the moment about that body's origin (the
              * HuntCrossleyForce record sums these per body, in ground) */
@@ -2957,13 +2982,13 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         }
         if constexpr (REP) {
             if (osim && a.osim_out)
-                osim_report<T, Real>(M, SM, lds, lane, D, control, t, istep, a.osim_out + (size_t)env * a.osim_dim);
+                osim_report<T, Real>(M, SM, lds, lane, D, control, t, istep, a.osim_out + GIDX((size_t)env, (size_t)N) * a.osim_dim);
         }
         wave_sync();
         if (obs)
-            for (int k = lane; k < M.obs_dim; k += G) obs[(size_t)env * a.obs_stride + k] = ob[k];
+            for (int k = lane; k < M.obs_dim; k += G) GAT(obs, (size_t)env * a.obs_stride + k, (size_t)N * a.obs_stride) = ob[k];
         if (a.final_obs && !reported_reset)
-            for (int k = lane; k < M.obs_dim; k += G) a.final_obs[(size_t)env * a.obs_stride + k] = ob[k];
+            for (int k = lane; k < M.obs_dim; k += G) GAT(a.final_obs, (size_t)env * a.obs_stride + k, (size_t)N * a.obs_stride) = ob[k];
         wave_sync();
         if (reported_reset || osim) break;
 
@@ -3055,14 +3080,14 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             done = d_;
         }
         if (lane == 0) {
-            if (a.reward) a.reward[env] = rew;
-            a.done_out[env] = (uint8_t)done;
+            if (a.reward) GAT(a.reward, env, N) = rew;
+            GAT(a.done_out, env, N) = (uint8_t)done;
         }
         if (a.info && lane < M.info_dim) {
             Real iv = inf[0];
 #pragma unroll
             for (int i = 1; i < 5; ++i) iv = lane == i ? inf[i] : iv;
-            a.info[(size_t)env * a.info_stride + lane] = iv;
+            GAT(a.info, (size_t)env * a.info_stride + lane, (size_t)N * a.info_stride) = iv;
         }
         wave_sync();
         if (done && a.auto_reset) {
@@ -3079,43 +3104,43 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
 #endif
     /* ---- store state */
         if (lane == 0) {
-        st.t[env] = t;
-        st.istep[env] = istep;
-        st.has_last[env] = has_last;
-        st.old_px[env] = old_px;
-        if (!osim) st.done[env] = (mode == 0 && !do_reset && !suspend) ? done : 0;
-        st.resets[env] = resets;
-        if (RK || mode == 1 || (osim && a.osim_op == BIOIM_OSIM_EQUILIBRATE)) st.hrk[env] = rk_hnext;
+        GAT(st.t, env, (size_t)N) = t;
+        GAT(st.istep, env, (size_t)N) = istep;
+        GAT(st.has_last, env, (size_t)N) = has_last;
+        GAT(st.old_px, env, (size_t)N) = old_px;
+        if (!osim) GAT(st.done, env, (size_t)N) = (mode == 0 && !do_reset && !suspend) ? done : 0;
+        GAT(st.resets, env, (size_t)N) = resets;
+        if (RK || mode == 1 || (osim && a.osim_op == BIOIM_OSIM_EQUILIBRATE)) GAT(st.hrk, env, (size_t)N) = rk_hnext;
         if constexpr (RK) {
-            st.pend[env] = suspend ? 1 : 0;
+            GAT(st.pend, env, (size_t)N) = suspend ? 1 : 0;
             /* evaluations: the attempts', plus one realize per finished step and per reset */
-            st.rkev[env] += launch_evals + (suspend ? 0 : 1) + (do_reset && mode == 0 ? 1 : 0);
-            if (a.traj && (mode == 0 || (osim && a.osim_op == BIOIM_OSIM_INTEGRATE))) a.traj_n[env] = traj_k;
+            GAT(st.rkev, env, (size_t)N) += launch_evals + (suspend ? 0 : 1) + (do_reset && mode == 0 ? 1 : 0);
+            if (a.traj && (mode == 0 || (osim && a.osim_op == BIOIM_OSIM_INTEGRATE))) GAT(a.traj_n, env, N) = traj_k;
             if (suspend) {
-                st.rkt[env] = rk_t; st.rkh[env] = rk_h; st.rka[env] = rk_attempts;
-                a.done_out[env] = 0;
+                GAT(st.rkt, env, (size_t)N) = rk_t; GAT(st.rkh, env, (size_t)N) = rk_h; GAT(st.rka, env, (size_t)N) = rk_attempts;
+                GAT(a.done_out, env, N) = 0;
             }
-            if (mode == 0 && a.ready_out) a.ready_out[env] = suspend ? 0 : 1;
+            if (mode == 0 && a.ready_out) GAT(a.ready_out, env, N) = suspend ? 0 : 1;
         }
     }
     if (RK && suspend) {
 #pragma unroll
         for (int j = 0; j < MPL; ++j) {
             const int m = mslot<T>(lane + j * G);
-            if (m < NA) st.cur[(size_t)m * N + env] = curr[j];
-            if (NM > 0 && m < NM) st.vnw[(size_t)m * N + env] = D.ms[j].vN;
+            if (m < NA) GAT(st.cur, (size_t)m * N + env, (size_t)NA * N) = curr[j];
+            if (NM > 0 && m < NM) GAT(st.vnw, (size_t)m * N + env, (size_t)(NM > 0 ? NM : 1) * N) = D.ms[j].vN;
         }
     }
     if (lane < ND) {
-        st.q[(size_t)lane * N + env] = qd;
-        st.u[(size_t)lane * N + env] = ud;
+        GAT(st.q, (size_t)lane * N + env, (size_t)ND * N) = qd;
+        GAT(st.u, (size_t)lane * N + env, (size_t)ND * N) = ud;
     }
 #pragma unroll
     for (int j = 0; j < MPL; ++j) {
         const int m = mslot<T>(lane + j * G);
-        if (NM > 0 && m < NM) { st.act[(size_t)m * N + env] = act[j]; st.lce[(size_t)m * N + env] = lce[j]; }
+        if (NM > 0 && m < NM) { GAT(st.act, (size_t)m * N + env, (size_t)(NM > 0 ? NM : 1) * N) = act[j]; GAT(st.lce, (size_t)m * N + env, (size_t)(NM > 0 ? NM : 1) * N) = lce[j]; }
         if (m < NA) {
-            st.last[(size_t)m * N + env] = last[j];
+            GAT(st.last, (size_t)m * N + env, (size_t)NA * N) = last[j];
         }
     }
 }
