@@ -38,7 +38,7 @@ pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLDEN_FILES = sorted(p for p in glob.glob(os.path.join(HERE, 'golden', '*.npz'))
-                      if not os.path.basename(p).startswith(('ik_', 'so_')))   # OpenSim pins: test_ik_pin.py, test_so_pin.py
+                      if not os.path.basename(p).startswith(('ik_', 'so_', 'drive_')))   # OpenSim pins (test_ik_pin.py, test_so_pin.py), drive schedules (tracking.py)
 TOL = 5e-9     # ~6x the oracle's own one-ulp twin at its worst step (see above)
 
 
