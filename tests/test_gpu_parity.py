@@ -671,7 +671,8 @@ def test_parity_200_steps_c3_tracking_drive():
     env.close()
 
 
-SCHEDULED_IDS = ['MuscleRunningImitation3D-v0', 'MuscleLockedKneeImitation3D-v0', 'MusclePalsyImitation3D-v0']
+SCHEDULED_IDS = ['MuscleRunningImitation3D-v0', 'MuscleLockedKneeImitation3D-v0', 'MusclePalsyImitation3D-v0',
+                 'MuscleWalkingImitation2D-v0']
 
 
 @pytest.mark.skipif(not gpu_available(), reason='needs GPU')
@@ -679,7 +680,9 @@ SCHEDULED_IDS = ['MuscleRunningImitation3D-v0', 'MuscleLockedKneeImitation3D-v0'
 def test_parity_200_steps_muscle_tracking_drive(env_id):
     """north_star on the spatial muscle configs (C4 Running3D, C5 LockedKnee3D
     and Palsy3D — the last passes the raw action to the physics,
-    muscle_palsy_imitation_env3D.py:131) with live envs: 200 identical-action
+    muscle_palsy_imitation_env3D.py:131) and on the headline C3 (Walking2D,
+    here from reference-rule rows instead of the hand-picked ones of
+    test_parity_200_steps_c3_tracking_drive) with live envs: 200 identical-action
     steps on 32 envs whose reset rows are drawn by the reference's rule
     (random.seed(0), random.randint(0, reset_hi); tools/drive_search.py), under
     the reference-tracking excitation drive of tests/tracking.py plus the

@@ -289,3 +289,77 @@ def test_02905_static_optimization_is_not_reproducible_from_its_shipped_inputs(o
     gy = z['grf'][:, :, 1].sum(1)
     flight = np.interp(z['so_time'], z['grf_time'], gy) < 5.0
     assert flight.sum() >= 10 and np.abs(fy[flight]).max() < 20.0
+
+
+def _swing_frames(so, side, h=0.02):
+    """SO frames where both of the leg's foot bodies (calcn, toes) are more
+    than h above the floor on our FK of the IK solution: that leg carries no
+    ground force, whatever the GRF file's labels say"""
+    B = so.names['bodies']
+    out = []
+    for t in so.z['so_time']:
+        _, p, _ = so.orc.fk(so._qd(so.q_spl(t)))
+        if min(p[B.index(f'calcn_{side}')][1], p[B.index(f'toes_{side}')][1]) > h:
+            out.append(t)
+    return np.array(out)
+
+
+def test_02905_swing_leg_rows_do_not_balance_either(oracle_lib):
+    """VERDICT r03 item 5 asked to pin the palsy model's muscles on the rows
+    that need no GRF: a leg in swing carries no ground force, so its hip /
+    knee / ankle rows of M q'' + c - g must equal its muscles' moments from
+    OpenSim's SO activations plus its reserves.  Finding: they do not, so
+    the 02905 run cannot pin the palsy muscles, not even there.
+    - During the left swing (1.38-1.63 s; calcn_l and toes_l > 2 cm above
+      the floor) the SO solution activates gastroc_l at 0.33 and soleus_l at
+      0.12 — about 80 N m of plantarflexion on a swinging foot whose
+      inverse-dynamics moment is 0.6 N m RMS: RMS(tau_ID - tau_SO) /
+      RMS(tau_ID) = 2.0 (hip flexion), 2.2 (hip adduction), 9.8 (knee),
+      101 (ankle).  The run therefore had a ground load on the left foot.
+    - Applying the wrench the run's own pelvis rows imply (6 equations, 6
+      unknowns) to calcn_l or to calcn_r leaves every leg row at 0.7-12.
+    - The run was made on ../scale/model_scaled.osim (setup_so.xml:5), which
+      has no explicit Millard curve parameters; the palsy env's
+      model_predictive.osim sets them (model_predictive.osim:1851-1870, e.g.
+      ActiveForceLengthCurve minimum_value 0), so no SO shipped with the
+      reference was solved with the curves the palsy env uses.
+    The palsy model's curves are pinned to their .osim parameters by the
+    model compiler tests (tests/test_modelpack.py) and exercised on the HIP
+    path by the golden and drive tests; the joint-level OpenSim pin stays the
+    3D trial's (mean 8.3 %)."""
+    z = dict(np.load(os.path.join(HERE, 'golden', 'so_02905.npz'), allow_pickle=False))
+    so = SOBalance(oracle_lib, z)
+    ts = _swing_frames(so, 'l')
+    assert len(ts) >= 20 and ts[0] > 1.3 and ts[-1] < 1.7, ts
+    assert len(_swing_frames(so, 'r')) == 0
+    names = so.names['coords']
+    left = [so.dof[names.index(c)] for c in ('hip_flexion_l', 'hip_adduction_l', 'knee_angle_l', 'ankle_angle_l')]
+    pel = [so.dof[names.index(c)] for c in PELVIS]
+    B = so.names['bodies']
+    tid0, tso = [], []
+    for t in ts:
+        qc, uc, ac = so.q_spl(t), so.q_spl.derivative(1)(t), so.q_spl.derivative(2)(t)
+        q, u, a = so._qd(qc), so._qd(uc), so._qd(ac)
+        tid0.append(so.orc.id_eval(2, q, u, a) + so.orc.id_eval(1, q, u) - so.orc.id_eval(0, q))
+        tso.append(so.frame(t)[1])
+    tid0, tso = np.array(tid0), np.array(tso)
+
+    def rel(tid, d):
+        return np.sqrt(np.mean((tid[:, d] - tso[:, d]) ** 2)) / np.sqrt(np.mean(tid[:, d] ** 2))
+    r = [rel(tid0, d) for d in left]
+    assert min(r) > 1.5 and r[3] > 50, r                    # measured 1.97 / 2.24 / 9.79 / 101
+    mus = list(z['so_names'])
+    i = np.searchsorted(z['so_time'], ts[len(ts) // 2] - 1e-9)
+    assert z['so_values'][i, mus.index('gastroc_l')] > 0.25     # a plantarflexor firing in swing
+    for foot in ('calcn_l', 'calcn_r'):
+        b = B.index(foot)
+        tid = []
+        for k, t in enumerate(ts):
+            q = so._qd(so.q_spl(t))
+            R0, p0 = so._frames(q)
+            Jv, Jw = so._body_jacobian(q, b, p0[b])
+            J = np.vstack([Jv, Jw])
+            W = np.linalg.solve(J[:, pel].T, tid0[k][pel] - tso[k][pel])
+            tid.append(tid0[k] - J.T @ W)
+        tid = np.array(tid)
+        assert min(rel(tid, d) for d in left) > 0.5, foot   # measured >= 0.72

@@ -40,13 +40,14 @@ def test_tracking_drive_keeps_the_listed_rows_up():
 
 
 @pytest.mark.parametrize('env_id', ['MuscleRunningImitation3D-v0', 'MuscleLockedKneeImitation3D-v0',
-                                    'MusclePalsyImitation3D-v0'])
+                                    'MusclePalsyImitation3D-v0', 'MuscleWalkingImitation2D-v0'])
 def test_scheduled_drive_premises(env_id):
     """The premises of test_gpu_parity.py::test_parity_200_steps_muscle_tracking_drive
     on the oracle: the committed schedule (tests/golden/drive_<ID>.npz) was
     found for reset rows drawn by the reference's rule (random.seed(0) +
     random.randint(0, reset_hi), tools/drive_search.py) and keeps >= 50 % of
-    the 32 envs alive for 200 steps; under it the dynamics are mostly not
+    the 32 envs alive for 200 steps or to the episode limit (istep >= N,
+    which rows drawn near reset_hi reach first); under it the dynamics are mostly not
     chaotic: on >= 3/4 of the envs a one-ulp twin stays within 1e-6 while
     both are alive (the GPU test bounds each env by its own twins)."""
     import random
@@ -66,7 +67,7 @@ def test_scheduled_drive_premises(env_id):
         orc.reset(bufs, i, int(r))
         orc.reset(twin, i, int(r))
         make_twin(orc, twin, i, 5)
-    alive, live = np.ones(n, bool), np.ones(n, bool)
+    alive, live, limit = np.ones(n, bool), np.ones(n, bool), np.zeros(n, bool)
     worst = np.zeros(n)
     for t in range(T):
         for i in np.where(alive)[0]:
@@ -76,6 +77,7 @@ def test_scheduled_drive_premises(env_id):
             if live[i]:
                 worst[i] = max(worst[i], (np.abs(o2 - o) / np.maximum(1.0, np.abs(o))).max())
             alive[i] = not d
+            limit[i] = d and orc.get_state(bufs, i)[1] >= pk.n_episode
             live[i] = live[i] and not (d or d2)
-    assert alive.sum() >= n // 2, alive.sum()
+    assert (alive | limit).sum() >= n // 2, (alive.sum(), limit.sum())
     assert (worst < 1e-6).sum() >= 3 * n // 4, worst
