@@ -40,7 +40,7 @@
 #include "topologies.h"
 
 #define DEV __device__ __forceinline__
-#define BIOIM_WG 256 /* threads per workgroup: 256 / G envs share one LDS model image */
+#define BIOIM_EPB 16 /* envs per workgroup (BIOIM_EPB * G threads) share one LDS model image */
 /* env flags baked into a kernel (topologies.h FLAGS); RAW_ACTION, TARGET_OBS, GRF_OBS are run-time */
 #define BIOIM_STRUCT_FLAGS (BIOIM_ENV_MUSCLE | BIOIM_ENV_HAS_TZ | BIOIM_ENV_REWARD_FEET | BIOIM_ENV_DONE_CROSS | BIOIM_ENV_PD)
 
@@ -2049,18 +2049,18 @@ template <class T, typename Real> struct IdArgs {
 
 template <class T, typename Real>
 #ifndef BIOIM_ID_NO_WAVES_ATTR
-__global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))) void id_kernel(IdArgs<T, Real> a) {
+__global__ __launch_bounds__(BIOIM_EPB * T::G) __attribute__((amdgpu_waves_per_eu(1, 1))) void id_kernel(IdArgs<T, Real> a) {
 #else   /* the compiler-crash reproducer (profiles/r03/regalloc_crash/): without the occupancy attribute */
-__global__ __launch_bounds__(BIOIM_WG) void id_kernel(IdArgs<T, Real> a) {
+__global__ __launch_bounds__(BIOIM_EPB * T::G) void id_kernel(IdArgs<T, Real> a) {
 #endif
     using LY = Lay<T, Real>;
-    constexpr int G = T::G, ND = LY::ND, NB = T::NB, NP = LY::NP, EPB = BIOIM_WG / G;
+    constexpr int G = T::G, ND = LY::ND, NB = T::NB, NP = LY::NP, EPB = BIOIM_EPB;
     constexpr size_t SMB = smodel_bytes<T, Real>();
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(a.Sg);
         uint4 *dst = reinterpret_cast<uint4 *>(smem_raw);
-        for (int i = threadIdx.x; i < (int)(SMB / 16); i += BIOIM_WG) dst[i] = src[i];
+        for (int i = threadIdx.x; i < (int)(SMB / 16); i += BIOIM_EPB * G) dst[i] = src[i];
     }
     __syncthreads();
     const SModel<T, Real> &SM = *reinterpret_cast<const SModel<T, Real> *>(smem_raw);
@@ -2462,7 +2462,7 @@ template <class T, typename Real, bool PERT, bool RK, bool REP>
 DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     using LY = Lay<T, Real>;
     constexpr int G = T::G, ND = LY::ND, NA = T::NA, NM = T::NM;
-    constexpr int EPB = BIOIM_WG / G;
+    constexpr int EPB = BIOIM_EPB;
     constexpr size_t SMB = smodel_bytes<T, Real>();
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const DModel<Real> *__restrict__ Mg = a.Mg;
@@ -2479,7 +2479,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(a.Sg);
         uint4 *dst = reinterpret_cast<uint4 *>(smem_raw);
-        for (int i = threadIdx.x; i < (int)(SMB / 16); i += BIOIM_WG) dst[i] = src[i];
+        for (int i = threadIdx.x; i < (int)(SMB / 16); i += BIOIM_EPB * G) dst[i] = src[i];
     }
     __syncthreads();
 #ifdef BIOIM_STAMPS
@@ -3149,7 +3149,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
  * the full realize report; separate instantiations, so the step kernels are
  * untouched by it */
 template <class T, typename Real, bool PERT, bool RK, bool REP = false>
-__global__ __launch_bounds__(BIOIM_WG) __attribute__((amdgpu_waves_per_eu(1, 1))) void env_kernel(LaunchArgs<T, Real> a) {
+__global__ __launch_bounds__(BIOIM_EPB * T::G) __attribute__((amdgpu_waves_per_eu(1, 1))) void env_kernel(LaunchArgs<T, Real> a) {
     env_block<T, Real, PERT, RK, REP>(a, blockIdx.x);
 }
 
@@ -3548,7 +3548,7 @@ struct OsimCall {   /* mode 2 launch arguments (bioim_osim) */
 
 struct Ops {
     int lanes;
-    size_t lds_bytes;   /* per workgroup: model image + BIOIM_WG / lanes env regions */
+    size_t lds_bytes;   /* per workgroup: model image + BIOIM_EPB env regions */
     int (*upload)(bioim_handle_t *);
     void (*launch)(bioim_handle_t *, int mode, const void *actions, void *obs, void *reward, uint8_t *done, void *info,
                    const int32_t *env_ids, const int32_t *ref_index, int n_list, const OsimCall *oc);
@@ -3587,8 +3587,8 @@ struct bioim_handle {
 namespace {
 
 template <class T, typename Real, bool PERT = false> constexpr size_t lds_bytes() {
-    return smodel_bytes<T, Real>() + (size_t)(BIOIM_WG / T::G) * Lay<T, Real>::SIZE * sizeof(Real) +
-           (PERT ? (size_t)(BIOIM_WG / T::G) * PERT_SLOT * sizeof(double) : 0);
+    return smodel_bytes<T, Real>() + (size_t)BIOIM_EPB * Lay<T, Real>::SIZE * sizeof(Real) +
+           (PERT ? (size_t)BIOIM_EPB * PERT_SLOT * sizeof(double) : 0);
 }
 
 /* bioim_osim_report_dim (include/bioim.h layout) */
@@ -3600,7 +3600,7 @@ template <class T, typename Real>
 LaunchArgs<T, Real> make_args(bioim_handle_t *h, int mode, const void *actions, void *obs, void *reward, uint8_t *done,
                               void *info, const int32_t *env_ids, const int32_t *ref_index, int n_list,
                               const OsimCall *oc) {
-    constexpr int EPB = BIOIM_WG / T::G;
+    constexpr int EPB = BIOIM_EPB;
     LaunchArgs<T, Real> a;
     const int count = mode != 0 ? n_list : h->n;
     a.Mg = reinterpret_cast<const DModel<Real> *>(h->model);
@@ -3646,7 +3646,7 @@ void launch_impl(bioim_handle_t *h, int mode, const void *actions, void *obs, vo
     /* the perturbation kernels are separate instantiations, so the default
      * kernels' code is untouched by the (rarely used) push */
     constexpr size_t lds0 = lds_bytes<T, Real, false>(), lds1 = lds_bytes<T, Real, true>();
-    const dim3 g(a.blocks), b(BIOIM_WG);
+    const dim3 g(a.blocks), b(BIOIM_EPB * T::G);
     if (mode == 2) {   /* OsimModel calls: the REP kernels */
         if (a.pert_n > 0 && h->rk) hipLaunchKernelGGL((env_kernel<T, Real, true, true, true>), g, b, lds1, h->stream, a);
         else if (a.pert_n > 0) hipLaunchKernelGGL((env_kernel<T, Real, true, false, true>), g, b, lds1, h->stream, a);
@@ -3662,7 +3662,7 @@ void launch_impl(bioim_handle_t *h, int mode, const void *actions, void *obs, vo
 
 template <class T, typename Real>
 void id_launch_impl(bioim_handle_t *h, int op, int n, const void *q, const void *u, const void *v, void *out) {
-    constexpr int EPB = BIOIM_WG / T::G;
+    constexpr int EPB = BIOIM_EPB;
     IdArgs<T, Real> a;
     a.Mg = reinterpret_cast<const DModel<Real> *>(h->model);
     a.Sg = reinterpret_cast<const SModel<T, Real> *>(h->smodel);
@@ -3670,7 +3670,7 @@ void id_launch_impl(bioim_handle_t *h, int op, int n, const void *q, const void 
     a.q = reinterpret_cast<const Real *>(q); a.u = reinterpret_cast<const Real *>(u);
     a.v = reinterpret_cast<const Real *>(v); a.out = reinterpret_cast<Real *>(out);
     constexpr size_t lds = lds_bytes<T, Real, false>();
-    hipLaunchKernelGGL((id_kernel<T, Real>), dim3((n + EPB - 1) / EPB), dim3(BIOIM_WG), lds, h->stream, a);
+    hipLaunchKernelGGL((id_kernel<T, Real>), dim3((n + EPB - 1) / EPB), dim3(BIOIM_EPB * T::G), lds, h->stream, a);
 }
 
 template <class T, typename Real> int upload_smodel(bioim_handle_t *h) {
@@ -4208,8 +4208,8 @@ int bioim_query(const bioim_handle_t *h, int32_t *out) {
 
 int bioim_query_launch(const bioim_handle_t *h, int32_t *out) {
     if (!h || !out) return fail(BIOIM_E_ARG, "bioim_query_launch: bad arguments");
-    const int epb = BIOIM_WG / h->ops.lanes;
-    out[0] = h->ops.lanes; out[1] = BIOIM_WG; out[2] = epb; out[3] = (int32_t)h->ops.lds_bytes;
+    const int epb = BIOIM_EPB;
+    out[0] = h->ops.lanes; out[1] = BIOIM_EPB * h->ops.lanes; out[2] = epb; out[3] = (int32_t)h->ops.lds_bytes;
     out[4] = (h->n + epb - 1) / epb;
     return 0;
 }

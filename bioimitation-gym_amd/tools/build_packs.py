@@ -129,7 +129,7 @@ def is_planar(pk):
     return pk.gravity[2] == 0
 
 
-def emit_topology(struct, pk, lanes):  # noqa: C901
+def emit_topology(struct, pk, lanes, lanes_expr=None):  # noqa: C901
     nb, nd, nc, nm = pk.ncbody, pk.ndof, pk.ncoord, pk.nmuscle
     parent = [pk.cbody[c].parent for c in range(nb)]
     anc = []
@@ -161,7 +161,7 @@ def emit_topology(struct, pk, lanes):  # noqa: C901
             axis_coord.append(-1 if fi < 0 else pk.fn[fi].coord)
     s = f'struct {struct} {{\n'
     s += f'    static constexpr int NB = {nb}, ND = {nd}, NC = {nc}, NM = {nm}, NA = {pk.nact}, NS = {pk.nsphere},' \
-         f' NF = {pk.ncforce}, NL = {pk.nlimit}, NOS = {pk.nosbody}, G = {lanes};\n'
+         f' NF = {pk.ncforce}, NL = {pk.nlimit}, NOS = {pk.nosbody}, G = {lanes_expr or lanes};\n'
     s += f'    static constexpr int NOBP = {pk.n_obs_bpos}, NOBV = {pk.n_obs_bvel};\n'
     s += f'    static constexpr int NPT = {pk.npathpt}, NFN = {pk.nfn}, NKNOT = {pk.nknots},' \
          f' NCURVE = {len(unique_curves(pk))},' \
@@ -240,7 +240,9 @@ def topology_signature(pk):
 
 def write_topologies(packs):
     out = ['/* GENERATED by tools/build_packs.py — compile-time topology of each env family. */',
-           '#pragma once', '']
+           '#pragma once', '',
+           '/* lanes per env of the spatial muscle topologies (16; 32 in the diagnostic G32 build) */',
+           '#ifndef BIOIM_G_SPATIAL_MUSCLE', '#define BIOIM_G_SPATIAL_MUSCLE 16', '#endif', '']
     names, seen = [], {}
     for env_id, pk in packs:
         # env IDs that differ only in env constants (e.g. Walking3D / Running3D) share one kernel
@@ -253,7 +255,12 @@ def write_topologies(packs):
         # 16 lanes per env (4 envs per wave): one lane per body, dof and reported body; muscles,
         # actions and coordinates beyond 16 take a second pass on the same lanes
         lanes = 16 if pk.ncbody < 16 and pk.ndof <= 16 and pk.nosbody < 16 else 32
-        out.append(emit_topology(struct, pk, lanes))
+        expr = None
+        if lanes == 16 and not is_planar(pk) and pk.nmuscle > 16:
+            # spatial muscle models (22 / 19 muscles: two muscle passes at 16 lanes); a diagnostic
+            # build sets BIOIM_G_SPATIAL_MUSCLE=32 (one muscle per lane, 512-thread workgroups)
+            expr = 'BIOIM_G_SPATIAL_MUSCLE'
+        out.append(emit_topology(struct, pk, lanes, expr))
         names.append((env_id, struct))
     out.append('#define BIOIM_FOR_EACH_TOPOLOGY(X) \\')
     out.append(' \\\n'.join(f'    X({s}, "{e}")' for e, s in names))
