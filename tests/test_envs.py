@@ -172,3 +172,39 @@ def test_single_env_save_simulation_and_perturbation(tmp_path):
     col = labels.index('/jointset/knee_r/knee_angle_r/value')
     np.testing.assert_allclose(data[:, col], [s[5 + pk.coord[c].dof] for s in states], atol=1e-8)
     env.close()
+
+
+def test_rllib_creator_dispatches_on_num_envs(monkeypatch):
+    """the Ray creator registered for an ID
+    (envs.rllib_creator; bioimitation/__init__.py:135-143 registers
+    ``lambda config: Env(config)``) returns the single-env class for the
+    reference's configs and one batched RLlibVectorEnv when the env config
+    asks for num_envs > 1 (device / precision passed through, the worker
+    index offsetting the global env indices).  Host logic only: both
+    constructors are replaced by recorders."""
+    from bioimitation import adapters, envs
+    calls = []
+
+    class Single:
+        def __init__(self, config=None):
+            calls.append(('single', dict(config or {})))
+
+    class Vec:
+        def __init__(self, env_id, num_envs, config=None, device=0, precision=64, seed=0, env_offset=0):
+            calls.append(('vec', env_id, num_envs, dict(config or {}), device, precision, env_offset))
+
+    class EnvContext(dict):          # ray.rllib.env.EnvContext: a dict with worker_index
+        worker_index = 3
+
+    env_id = 'MuscleWalkingImitation2D-v0'
+    monkeypatch.setitem(envs.ENV_CLASSES, env_id, Single)
+    monkeypatch.setattr(adapters, 'RLlibVectorEnv', Vec)
+    create = envs.rllib_creator(env_id)
+    create({'mode': 'test'})
+    create(EnvContext(num_envs=1, horizon=3))
+    create(EnvContext(num_envs=256, device=1, precision=32, horizon=3))
+    assert calls[0] == ('single', {'mode': 'test'})
+    assert calls[1] == ('single', {'num_envs': 1, 'horizon': 3})
+    assert calls[2] == ('vec', env_id, 256, {'horizon': 3}, 1, 32, 3 * 256)
+    with pytest.raises(NotImplementedError):
+        envs.rllib_creator('MuscleJumpingImitation2D-v0')
