@@ -132,8 +132,7 @@ class ImitationEnv:
         """o: the env's observation row on the host"""
         if self._record:
             fr = self._env.force_report[0].double().cpu().numpy()
-            self.osim_model.recorder.record(self._env.get_state()[0], o[self._qdd], fr,
-                                            storage=self.osim_model.storage() if stepped else None)
+            self.osim_model.record_row(self._env.get_state()[0], o[self._qdd], fr, stepped)
 
     def reset(self, obs_as_dict=False):
         index = 0 if self.test else random.randint(0, self._env.pack.reset_hi)
@@ -231,6 +230,7 @@ class ImitationEnv:
         return [s]
 
     def close(self):
+        self.osim_model.close()
         self._env.close()
 
 

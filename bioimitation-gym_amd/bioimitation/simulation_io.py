@@ -99,6 +99,16 @@ class TrajectoryRecorder:
                 self.state_rows.append(self._full(r[0], r[1:1 + nd], r[1 + nd:1 + 2 * nd], r[1 + 2 * nd:1 + 2 * nd + nm],
                                                   r[1 + 2 * nd + nm:1 + 2 * nd + 2 * nm]))
 
+    def record_steps(self, state_rows, qdd_rows, force_rows):
+        """One analysis row and one Manager state row per accepted
+        integration step (RK mode): OpenSim's Manager stores the state after
+        every accepted step and its analyses (Kinematics, ForceReporter;
+        step_interval 1) record at the same states (opensim_wrapper.py:10-15,
+        :336).  state_rows: the flat states (include/bioim.h layout) of the
+        accepted steps; qdd_rows / force_rows: their realizations."""
+        for s, qdd, f in zip(state_rows, qdd_rows, force_rows):
+            self.record(s, qdd, f)
+
     # ------------------------------------------------------------------ output
     def _split(self):
         a = np.array(self.rows) if self.rows else np.zeros((0, 1 + 3 * self.nc + 2 * self.pack.nmuscle))
@@ -424,6 +434,56 @@ class OsimModelFacade:
             k = cap
         return env.storage_rows[self._i, :k].double().cpu().numpy()
 
+    def _realizer(self, k):
+        """a batch of the same model (one env per stored state) on which the
+        accepted integration steps are realized; grown on demand"""
+        rz = getattr(self, '_rz', None)
+        if rz is None or rz.num_envs < k:
+            from .vector_env import VectorEnv
+            e = self._env
+            if rz is not None:
+                rz.close()
+            rz = VectorEnv(e.env_id, max(k, 64), config=e.config, device=e.device.index, precision=e.precision)
+            rz.enable_force_report()
+            self._rz = rz
+        return rz
+
+    def analysis_rows(self, storage):
+        """(states, q'' rows, ForceReporter rows) at the accepted integration
+        steps of the last env step: each stored state (t, q, u, activation,
+        fiber length; bioim_set_state_storage) is put into this env's state
+        row — so the step's held controls come with it — and realized on a
+        scratch batch (bioim_osim realize, the REP kernels), one env per row."""
+        pk = self._pack
+        nd, nm = pk.ndof, pk.nmuscle
+        k = len(storage)
+        rz = self._realizer(k)
+        S = np.tile(self._state()[self._i], (rz.num_envs, 1))
+        st = np.asarray(storage, dtype=np.float64)
+        S[:k, 0] = st[:, 0]
+        S[:k, 5:5 + 2 * nd + 2 * nm] = st[:, 1:1 + 2 * nd + 2 * nm]   # q u act lce: the same order
+        rz.set_state(S)
+        rep = rz.osim('realize', list(range(k)), want_obs=False)[:k].double().cpu().numpy()
+        qdd = [split_osim_report(pk, r)['qdd'] for r in rep]
+        return S[:k], qdd, rz.force_report[:k].double().cpu().numpy()
+
+    def close(self):
+        rz = getattr(self, '_rz', None)
+        if rz is not None:
+            rz.close()
+            self._rz = None
+
+    def record_row(self, state_row, qdd, force_row, stepped=True):
+        """the analyses' rows of one env step: with the reference's integrator,
+        one per accepted integration step (analysis_rows); otherwise the end
+        state (one per 0.01 s)"""
+        storage = self.storage() if stepped else None
+        if storage is not None:
+            if len(storage):
+                self.recorder.record_steps(*self.analysis_rows(storage))
+            return
+        self.recorder.record(state_row, qdd, force_row)
+
     def _record(self, stepped=True):
         """one analysis row: the state, q'' of the realize and the ForceReporter
         row (``bioim_set_force_report``, the same full row ImitationEnv records:
@@ -433,8 +493,7 @@ class OsimModelFacade:
             env.enable_force_report()
             self._call('realize')          # fills the force row of the current state
         r = self.report()
-        self.recorder.record(self._state()[self._i], r['qdd'], env.force_report[self._i].double().cpu().numpy(),
-                             storage=self.storage() if stepped else None)
+        self.record_row(self._state()[self._i], r['qdd'], env.force_report[self._i].double().cpu().numpy(), stepped)
 
     # ------------------------------------------------------------ realizations
     def calc_joint_kinematics(self):

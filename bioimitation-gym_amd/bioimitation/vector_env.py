@@ -56,6 +56,7 @@ class VectorEnv:
             raise _lib.BioimError('VectorEnv needs a HIP GPU (no CPU fallback)')
         L = _lib.load()
         self.env_id = env_id
+        self.config = dict(config or {})
         self.pack = load_pack(env_id, config)
         self.num_envs = int(num_envs)
         self.device = torch.device('cuda', device)

@@ -298,3 +298,56 @@ def test_rk_state_storage_rows_match_oracle(tmp_path):
     np.testing.assert_allclose(data[1:, col], rows_orc[:, 1 + 2 * pk.ndof + pk.nmuscle], rtol=1e-6, atol=1e-8)
     assert len(rows_orc) > 6 * 3        # several accepted steps per 0.01 s env step
     env.close()
+
+
+def test_rk_analyses_record_every_integration_step(tmp_path):
+    """With the reference's integrator OpenSim's Kinematics and ForceReporter
+    analyses record at every accepted integration step, like the Manager's
+    state storage (opensim_wrapper.py:10-15, :334-338).  Each of the GPU's
+    stored states (the same rows as the oracle's: test above) is realized
+    with the step's held controls (OsimModelFacade.analysis_rows, bioim_osim
+    on a scratch batch): q'' and the ForceReporter row per accepted step equal
+    the oracle's realize of the oracle's stored states (1e-6 relative to
+    max(|x|, 1): the step sizes agree to the rounding level, q'' near contact
+    carries its conditioning), and the four .sto files hold one row per
+    accepted step plus the initial state."""
+    import oracle
+    from bioimitation import envs
+    from bioimitation.simulation_io import split_osim_report
+    from bioimitation.storage import read_sto
+    env_id = 'MuscleWalkingImitation2D-v0'
+    env = envs.make(env_id, config={'integrator': 'rk-merson', 'mode': 'test'})
+    env.reset()
+    pk = env._env.pack
+    nd, nm = pk.ndof, pk.nmuscle
+    orc = oracle.Oracle(pk)
+    bufs, scratch = orc.new_envs(1), orc.new_envs(1)
+    orc.set_integrator(bufs, 0, 'rk-merson', 1e-3)
+    orc.reset(bufs, 0, 0)
+    store = np.zeros((512, 1 + 2 * nd + 2 * nm))
+    orc.set_state_storage(bufs, 0, store)
+    rng = np.random.default_rng(4)
+    want_qdd, want_f = [], []
+    for t in range(5):
+        a = rng.uniform(0.0, 0.6, size=pk.nact)
+        env.step(a)
+        orc.step(bufs, 0, a)
+        base = orc.get_state(bufs, 0)
+        for r in store[:orc.state_storage_count(bufs, 0)]:
+            s = base.copy()
+            s[0] = r[0]
+            s[5:5 + 2 * nd + 2 * nm] = r[1:]
+            orc.set_state(scratch, 0, s)
+            want_qdd.append(split_osim_report(pk, orc.osim_report(scratch, 0))['qdd'])
+            want_f.append(orc.force_report(scratch, 0))
+    rec = env.osim_model.recorder
+    nc = pk.ncoord
+    got_qdd = np.array([r[1 + 2 * nc:1 + 3 * nc] for r in rec.rows[1:]])
+    got_f = np.array([r[1:] for r in rec.force_rows[1:]])
+    assert len(got_qdd) == len(want_qdd) > 5 * 3, (len(got_qdd), len(want_qdd))
+    np.testing.assert_allclose(got_qdd, np.array(want_qdd), rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(got_f, np.array(want_f), rtol=1e-6, atol=1e-6)
+    paths = env.osim_model.save_simulation(str(tmp_path))
+    for key in ('states', 'q', 'u', 'dudt', 'forces'):
+        assert len(read_sto(paths[key])[2]) == 1 + len(want_qdd), key
+    env.close()
