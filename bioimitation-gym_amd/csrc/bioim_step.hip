@@ -2342,7 +2342,11 @@ DEV void osim_report(const DModel<Real> &M, const SModel<T, Real> &SM, const Rea
     constexpr int OLIM = OCF + 6 * T::NF, OCOT = OLIM + T::NL;
     const Real x0 = D.x0;
     if (lane == 0) { out[0] = Real(t); out[1] = Real(istep); }
-#pragma unroll
+    /* loops over bodies, spheres and coordinates run rolled (unroll 1): the
+     * report is off the stepping path, and unrolled it held every body's terms
+     * live at the kernel's peak register pressure — 0.6-2.9 KB/lane of scratch
+     * in the REP kernels before (profiles/r03/resources.txt) */
+#pragma unroll 1
     for (int jc = 0; jc < CPL; ++jc) {
         const int c = lane + jc * G;
         if (c < NC) {
@@ -2393,7 +2397,7 @@ DEV void osim_report(const DModel<Real> &M, const SModel<T, Real> &SM, const Rea
         }
     } else if (lane == NOS) {
         Real mt = 0, cs[3] = {0, 0, 0}, vs[3] = {0, 0, 0}, as[3] = {0, 0, 0};
-#pragma unroll
+#pragma unroll 1
         for (int c = 0; c < T::NB; ++c) {
             const Real *kb = lds + LY::KB + 18 * c;
             Real cG[3], vc[3], ac[3], tt[3], t2[3], al[3], aO[3];
@@ -2438,7 +2442,7 @@ DEV void osim_report(const DModel<Real> &M, const SModel<T, Real> &SM, const Rea
     }
     if (lane < T::NF) {
         Real F[3] = {0, 0, 0}, Mo[3] = {0, 0, 0};
-#pragma unroll
+#pragma unroll 1
         for (int s2 = 0; s2 < T::NS; ++s2) {
             const Real *cw = lds + LY::CW + 8 * s2;
             const bool mine = SM.sph_force[s2] == lane;
