@@ -86,6 +86,11 @@ DEV void sfor(F &&f) {
 #ifndef BIOIM_BF_SPATIAL
 #define BIOIM_BF_SPATIAL 0
 #endif
+/* BIOIM_BF3_RK=1: the BIOIM_BF3 pieces in the spatial RK-Merson kernels too
+ * (an A/B variant; off in the shipped build) */
+#ifndef BIOIM_BF3_RK
+#define BIOIM_BF3_RK 0
+#endif
 template <typename Real> struct Eps;
 template <> struct Eps<float> {
     static constexpr float u_tol = 2e-7f;   /* Bezier parameter tolerance  */
@@ -1659,7 +1664,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
      * kernels (BIOIM_BF3 bits: 1 function slots, 2 muscle paths, 4 contact,
      * 8 limits, 16 fiber equilibrium, 32 phase-3 rows, 64 implicit
      * terms without a branch on h, 128 muscle eval) */
-    constexpr bool BF3 = !T::PLANAR && IMP;
+    constexpr bool BF3 = !T::PLANAR && (IMP || BIOIM_BF3_RK);
     constexpr bool BFK_FN = BFK || (BF3 && (BIOIM_BF3 & 1)), BFK_PATH = BFK || (BF3 && (BIOIM_BF3 & 2));
     constexpr bool BFK_CON = BFK || (BF3 && (BIOIM_BF3 & 4)), BFK_LIM = BFK || (BF3 && (BIOIM_BF3 & 8));
     constexpr bool BFK_EQ = BFK || (BF3 && (BIOIM_BF3 & 16)), BFK_ROW = BFK || (BF3 && (BIOIM_BF3 & 32));
