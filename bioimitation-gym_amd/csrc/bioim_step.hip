@@ -86,10 +86,11 @@ DEV void sfor(F &&f) {
 #ifndef BIOIM_BF_SPATIAL
 #define BIOIM_BF_SPATIAL 0
 #endif
-/* BIOIM_BF3_RK=1: the BIOIM_BF3 pieces in the spatial RK-Merson kernels too
- * (an A/B variant; off in the shipped build) */
+/* BIOIM_BF3_RK=1 (shipped): the BIOIM_BF3 pieces in the spatial RK-Merson
+ * kernels too — no scratch, hazard gate clean, same-box Running3D RK launch
+ * 0.7826 -> 0.7452 ms, LockedKnee3D 0.7289 -> 0.6989 ms (profiles/r04/r04g/ab_rk.log) */
 #ifndef BIOIM_BF3_RK
-#define BIOIM_BF3_RK 0
+#define BIOIM_BF3_RK 1
 #endif
 template <typename Real> struct Eps;
 template <> struct Eps<float> {
@@ -1658,7 +1659,8 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
      * kernels, except the torque-model RK ones: an RK build of these forms
      * put a lane-divergent copy of a live-in-all-lanes address into an AGPR
      * in the Torque2D RK kernel and faulted; that kernel
-     * keeps the GPU-verified code, and tools/hazard_gate.py checks the others */
+     * keeps the GPU-verified code (round 4: the same forms there again give 4
+     * flagged copies in tools/hazard_gate.py), and the gate checks the others */
     constexpr bool BFK = (T::PLANAR || BIOIM_BF_SPATIAL) && (IMP || T::NM > 0);
     /* per-piece switches of the branch-free forms in the spatial semi-implicit
      * kernels (BIOIM_BF3 bits: 1 function slots, 2 muscle paths, 4 contact,
