@@ -80,6 +80,7 @@ def main():
         sq = sq_summary(os.path.join(ev, f'pmc_{k}'))
         if sq:
             rec = valu.record(sq, ms, src)
+            rec.update(valu.issue_analysis(sq, ms))
             rec['build_id'] = bid
             vdb[key] = rec
             with open(os.path.join(ev, f'{k}_fp64_pmc_sq_summary.txt'), 'w') as fh:

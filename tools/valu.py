@@ -43,6 +43,27 @@ def record(v, kernel_ms, source):
             'kernel_ms': kernel_ms, 'source': source}
 
 
+def issue_analysis(v, kernel_ms, waves=1024, clock_ghz=2.4):
+    """VALU issue against its ceiling and where the other wave cycles go.
+    One wave alone on its SIMD issues a VALU instruction per 4 cycles (8 for
+    a transcendental; MI355X_MICROARCH.md constants, 'vector-instruction
+    ISSUE cost'), so the kernel's issue floor is its VALU instructions per
+    wave x 4 cycles; the SQ shares are fractions of SQ_WAVE_CYCLES:
+    ACTIVE_INST_ANY (some instruction issuing), WAIT_INST_ANY (at an
+    s_waitcnt: LDS / memory), and the residual — cycles with no instruction
+    issued and no waitcnt — which is the dependent-instruction latency of
+    the wave's own VALU chain (no SQ counter of its own)."""
+    per_wave = (v['SQ_INSTS_VALU'] + v.get('SQ_INSTS_VALU_TRANS_F64', 0) + v.get('SQ_INSTS_VALU_TRANS_F32', 0)) / waves
+    floor_cycles = 4.0 * per_wave
+    kernel_cycles = kernel_ms * 1e-3 * clock_ghz * 1e9
+    w = v['SQ_WAVE_CYCLES']
+    return {'valu_issue_floor_us': floor_cycles / (clock_ghz * 1e3), 'issue_ceiling_frac': floor_cycles / kernel_cycles,
+            'wave_cycle_shares': {'valu_issuing': v['SQ_ACTIVE_INST_VALU'] / w, 'any_issuing': v['SQ_ACTIVE_INST_ANY'] / w,
+                                  'waitcnt': v['SQ_WAIT_INST_ANY'] / w, 'waitcnt_lds': v['SQ_WAIT_INST_LDS'] / w,
+                                  'dependency_residual': 1.0 - (v['SQ_ACTIVE_INST_ANY'] + v['SQ_WAIT_INST_ANY']) / w},
+            'waves': waves, 'clock_ghz': clock_ghz}
+
+
 def main():
     summ, kms, env_id, prec, n, source = sys.argv[1:7]
     rec = record(read_summary(summ), float(kms), source)
