@@ -12,23 +12,23 @@ from conftest import gpu_available
 pytestmark = pytest.mark.gpu
 
 
-def _run_sync(env_id, n, T, acts, rows):
+def _run_sync(env_id, n, T, acts, rows, precision=64):
     import torch
     from bioimitation.vector_env import VectorEnv
-    env = VectorEnv(env_id, n, config={'integrator': 'rk-merson'}, precision=64)
+    env = VectorEnv(env_id, n, config={'integrator': 'rk-merson'}, precision=precision)
     env.reset(ref_index=rows)
     out = []
     for k in range(T):
-        o, r, d, _ = env.step(torch.as_tensor(acts[k], device=env.device))
+        o, r, d, _ = env.step(torch.as_tensor(acts[k], device=env.device, dtype=env.dtype))
         out.append((o.cpu().numpy().copy(), r.cpu().numpy().copy(), d.cpu().numpy().copy()))
     env.close()
     return out
 
 
-def _run_budget(env_id, n, T, acts, rows, budget):
+def _run_budget(env_id, n, T, acts, rows, budget, precision=64):
     import torch
     from bioimitation.vector_env import VectorEnv
-    env = VectorEnv(env_id, n, config={'integrator': 'rk-merson'}, precision=64)
+    env = VectorEnv(env_id, n, config={'integrator': 'rk-merson'}, precision=precision)
     env.set_rk_budget(budget)
     env.reset(ref_index=rows)
     k = np.zeros(n, dtype=int)
@@ -38,7 +38,7 @@ def _run_budget(env_id, n, T, acts, rows, budget):
     launches = suspended = 0
     while k.min() < T and launches < 40 * T:
         a = np.stack([acts[min(k[i], T - 1)][i] for i in range(n)])
-        o, r, d, _ = env.step(torch.as_tensor(a, device=env.device))
+        o, r, d, _ = env.step(torch.as_tensor(a, device=env.device, dtype=env.dtype))
         ready = env.ready.cpu().numpy().astype(bool)
         o, r, d = o.cpu().numpy(), r.cpu().numpy(), d.cpu().numpy()
         for i in np.nonzero(ready & (k < T))[0]:
@@ -52,8 +52,14 @@ def _run_budget(env_id, n, T, acts, rows, budget):
 
 
 @pytest.mark.skipif(not gpu_available(), reason='needs a HIP GPU')
-@pytest.mark.parametrize('env_id,budget', [('MuscleRunningImitation3D-v0', 6), ('TorqueWalkingImitation2D-v0', 4)])
-def test_rk_budget_equals_unbudgeted(env_id, budget):
+@pytest.mark.parametrize('env_id,budget,precision', [('MuscleRunningImitation3D-v0', 6, 64),
+                                                     ('TorqueWalkingImitation2D-v0', 4, 64),
+                                                     # fp32 RK kernels through the resume path (the
+                                                     # fp32 Muscle2D RK kernel is the one the round-3 gate let
+                                                     # carry flagged copies)
+                                                     ('MuscleWalkingImitation2D-v0', 6, 32),
+                                                     ('TorqueWalkingImitation2D-v0', 4, 32)])
+def test_rk_budget_equals_unbudgeted(env_id, budget, precision):
     from bioimitation.registry import load_pack
     pk = load_pack(env_id)
     n, T = 48, 12
@@ -64,9 +70,9 @@ def test_rk_budget_equals_unbudgeted(env_id, budget):
     else:
         acts = np.stack([np.array([[pk.ref_q[min(int(r) + k + 1, pk.nrows - 1)][pk.pd_coord[a]] for a in range(pk.nact)]
                                    for r in rows]) for k in range(T)]) + rng.normal(0, 0.05, size=(T, n, pk.nact))
-    ref = _run_sync(env_id, n, T, acts, rows)
-    o, r, d, launches, suspended, pending, k = _run_budget(env_id, n, T, acts, rows, budget)
-    print(f'{env_id}: budget {budget} attempts, {launches} launches for {T} steps, {suspended} suspensions, '
+    ref = _run_sync(env_id, n, T, acts, rows, precision)
+    o, r, d, launches, suspended, pending, k = _run_budget(env_id, n, T, acts, rows, budget, precision)
+    print(f'{env_id} fp{precision}: budget {budget} attempts, {launches} launches for {T} steps, {suspended} suspensions, '
           f'{pending} pending at the end')
     assert (k >= T).all(), k
     assert suspended > 0, 'the budget never suspended an env: the test does not exercise the resume path'
@@ -108,7 +114,7 @@ def _sync_reference(env_id, n, T, acts, integrator, seed):
     o0 = env.reset().cpu().numpy().copy()
     out = []
     for k in range(T):
-        o, r, d, _ = env.step(torch.as_tensor(acts[k], device=env.device))
+        o, r, d, _ = env.step(torch.as_tensor(acts[k], device=env.device, dtype=env.dtype))
         out.append((o.cpu().numpy().copy(), r.cpu().numpy().copy(), d.cpu().numpy().copy()))
     env.close()
     return o0, out
