@@ -86,10 +86,6 @@ DEV void sfor(F &&f) {
 #ifndef BIOIM_BF_SPATIAL
 #define BIOIM_BF_SPATIAL 0
 #endif
-/* BIOIM_FV_HALLEY=1: Halley's method in the fiber-velocity solve (A/B variant) */
-#ifndef BIOIM_FV_HALLEY
-#define BIOIM_FV_HALLEY 0
-#endif
 /* BIOIM_BF3_RK=1 (shipped): the BIOIM_BF3 pieces in the spatial RK-Merson
  * kernels too — no scratch, hazard gate clean, same-box Running3D RK launch
  * 0.7826 -> 0.7452 ms, LockedKnee3D 0.7289 -> 0.6989 ms (profiles/r04/r04g/ab_rk.log) */
@@ -103,7 +99,6 @@ template <> struct Eps<float> {
     static constexpr float v_tol = 1e-7f;   /* normalized velocity         */
     static constexpr float l_tol = 1e-9f;   /* fiber length (m)            */
     static constexpr float l_stop = 1e-9f;  /* Newton step after which the length is converged */
-    static constexpr float u_stop3 = 1e-3f; /* Halley step after which the root is converged */
     static constexpr int it_max = 24;
     static constexpr int curve_newton = 1; /* from the Hermite start: 5.9e-9 < fp32 rounding */
 };
@@ -115,9 +110,6 @@ template <> struct Eps<double> {
     static constexpr double v_tol = 1e-15;
     static constexpr double l_tol = 1e-15;
     static constexpr double l_stop = 1e-10;
-    /* a Halley step of at most 1e-6 leaves an error ~ C 1e-18 in u (cubic
-     * convergence; C = O(10) for the shipped curves) */
-    static constexpr double u_stop3 = 1e-6;
     static constexpr int it_max = 60;
     static constexpr int curve_newton = 2; /* from the Hermite start: 8.9e-16 */
 };
@@ -450,9 +442,6 @@ template <typename Real> DEV Real bez5(const Real *c, Real u) {
 template <typename Real> DEV Real dbez5(const Real *c, Real u) {
     return fma(fma(fma(fma(Real(5) * c[5], u, Real(4) * c[4]), u, Real(3) * c[3]), u, Real(2) * c[2]), u, c[1]);
 }
-template <typename Real> DEV Real ddbez5(const Real *c, Real u) {
-    return fma(fma(fma(Real(20) * c[5], u, Real(12) * c[4]), u, Real(6) * c[3]), u, Real(2) * c[2]);
-}
 
 /* y(x), dy/dx of a SmoothSegmentedFunction.  Branch-free with a fixed trip
  * count (no lane divergence): segment located by comparisons, u(x) started
@@ -552,27 +541,14 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
         Real g = bez5(pg, u);
         if (g > 0) hi = u; else lo = u;
         Real dg = dbez5(pg, u);
-#if BIOIM_FV_HALLEY
-        /* Halley's step (cubic convergence): one iteration fewer from the
-         * warm start than Newton's, for a short extra chain (g'' is
-         * evaluated beside g and g') */
-        Real d2g = ddbez5(pg, u);
-        Real un = u - Real(2) * g * dg * newton_rcp(fma(Real(2) * dg, dg, -g * d2g));
-#else
         Real un = u - g * newton_rcp(dg);
-#endif
         /* inclusive bracket: a converged step (un == u == lo or hi after
          * rounding) must not trigger the bisection fallback */
         if (!(un >= lo && un <= hi)) un = Real(0.5) * (lo + hi);
         Real du = fabs(un - u);
         u = un;
         /* converged, or stagnating at the rounding level of g */
-#if BIOIM_FV_HALLEY
-        constexpr Real ustop = Eps<Real>::u_stop3;
-#else
-        constexpr Real ustop = Eps<Real>::u_stop;
-#endif
-        if (it >= 1 && (du <= ustop || (du <= Real(1e3) * Eps<Real>::u_tol && du >= Real(0.5) * dprev))) {
+        if (it >= 1 && (du <= Eps<Real>::u_stop || (du <= Real(1e3) * Eps<Real>::u_tol && du >= Real(0.5) * dprev))) {
 #ifdef BIOIM_STAMPS
             if (blockIdx.x == 0 && threadIdx.x < 14) atomicAdd(&g_stamps[12], (unsigned long long)(it + 1));
             if (blockIdx.x == 0 && threadIdx.x < 14) atomicAdd(&g_stamps[13], 1ull);
