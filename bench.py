@@ -207,6 +207,8 @@ def main():
     ap.add_argument('--mixed', default=None,
                     help="mixed batch 'ID_A,ID_B' split 50/50 per GPU (BASELINE config C5), e.g. "
                          "MuscleLockedKneeImitation3D-v0,MusclePalsyImitation3D-v0")
+    ap.add_argument('--no-fuse', action='store_true',
+                    help='mixed batch: concurrent per-segment launches instead of the fused two-topology kernel')
     a = ap.parse_args()
     if a.rk_budget and (a.integrator != 'rk-merson' or a.mixed):
         ap.error('--rk-budget needs --integrator rk-merson and a single env id')
@@ -235,6 +237,8 @@ def main():
 
     from bioimitation.vector_env import MixedVectorEnv, VectorEnv
     if a.mixed:
+        from bioimitation import _lib
+        _lib.load().bioim_set_group_fusion(0 if a.no_fuse else 1)
         ids = a.mixed.split(',')
         sizes = [a.envs // len(ids)] * len(ids)
         sizes[-1] += a.envs - sum(sizes)
@@ -338,7 +342,7 @@ def main():
                        (f'nsub={env.nsub}' if a.integrator == 'semi-implicit' else 'RK-Merson 1e-3') + ', auto-reset',
                        'integrator': a.integrator, 'rk_budget': a.rk_budget or None,
                        'envs_per_gpu': n, 'lanes_per_env': env.lanes_per_env, 'parallelism': f'env-shard x{world}',
-                       'launch': env.launch},
+                       'launch': env.launch, **({'group_fusion': not a.no_fuse} if a.mixed else {})},
             'roofline': roofline,
         }
         valu = _profile_record('valu.json', key, build_id)

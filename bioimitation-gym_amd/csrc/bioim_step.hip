@@ -3172,14 +3172,34 @@ __global__ __launch_bounds__(BIOIM_EPB * T::G) __attribute__((amdgpu_waves_per_e
 }
 
 
+/* Fused two-topology step (a mixed batch, config C5, in ONE launch):
+ * workgroups [0, a0.blocks) step segment 0 with topology T0, the rest segment
+ * 1 with T1.  Both segments are the default step kernels' code (no push
+ * table, semi-implicit); the two bodies sit in one kernel, so its registers
+ * are the larger of the two (the 3D pair: 462, no scratch, hazard gate clean).
+ * Instantiated for the pairs in BIOIM_FUSED_PAIRS, in the library's fused
+ * unit (-DBIOIM_FUSED_ONLY). */
+template <class T0, class T1, typename Real>
+__global__ __launch_bounds__(BIOIM_EPB * T0::G) __attribute__((amdgpu_waves_per_eu(1, 1))) void env_kernel2(
+    LaunchArgs<T0, Real> a0, LaunchArgs<T1, Real> a1) {
+    static_assert(T0::G == T1::G, "a fused launch needs one workgroup shape");
+    if ((int)blockIdx.x < a0.blocks) env_block<T0, Real, false, false, false>(a0, blockIdx.x);
+    else env_block<T1, Real, false, false, false>(a1, blockIdx.x - a0.blocks);
+}
+
+#define BIOIM_FUSED_PAIRS(X)                                                         \
+    X(Topo_MuscleLockedKneeImitation3D_v0, Topo_MuscleWalkingImitation3D_v0)          \
+    X(Topo_MuscleWalkingImitation3D_v0, Topo_MuscleLockedKneeImitation3D_v0)
+
 /* =================================================================== host
  * Build modes (the library links 8 objects compiled in parallel):
  *   BIOIM_TOPO_ONLY=k  the kernels and host launchers of topology k only
  *                      (bioim_pick_k);
  *   BIOIM_ABI_ONLY     the C-ABI, no kernels;
+ *   BIOIM_FUSED_ONLY   the fused two-topology kernels (BIOIM_FUSED_PAIRS) and their launcher;
  *   neither            everything in one translation unit (diagnostic builds). */
-#if defined(BIOIM_TOPO_ONLY) && defined(BIOIM_ABI_ONLY)
-#error "BIOIM_TOPO_ONLY and BIOIM_ABI_ONLY are exclusive"
+#if defined(BIOIM_TOPO_ONLY) + defined(BIOIM_ABI_ONLY) + defined(BIOIM_FUSED_ONLY) > 1
+#error "BIOIM_TOPO_ONLY, BIOIM_ABI_ONLY and BIOIM_FUSED_ONLY are exclusive"
 #endif
 extern thread_local std::string g_err;   /* bioim_last_error(); defined with the C-ABI */
 
@@ -3565,6 +3585,7 @@ struct OsimCall {   /* mode 2 launch arguments (bioim_osim) */
 };
 
 struct Ops {
+    const char *topo;   /* the topology struct's name (fused-pair lookup) */
     int lanes;
     size_t lds_bytes;   /* per workgroup: model image + BIOIM_EPB env regions */
     int (*upload)(bioim_handle_t *);
@@ -3678,6 +3699,33 @@ void launch_impl(bioim_handle_t *h, int mode, const void *actions, void *obs, vo
     else hipLaunchKernelGGL((env_kernel<T, Real, false, false>), g, b, lds0, h->stream, a);
 }
 
+/* one launch of env_kernel2 for the segments h0 (rows [0, n0)) and h1 (the
+ * rows after them) of a group step; on h0's stream */
+template <class T0, class T1, typename Real>
+int fused_launch_impl(bioim_handle_t *h0, bioim_handle_t *h1, const void *actions, void *obs, void *reward,
+                      uint8_t *done, void *info) {
+    constexpr size_t R = sizeof(Real);
+    const size_t n0 = (size_t)h0->n;
+    LaunchArgs<T0, Real> a0 = make_args<T0, Real>(h0, 0, actions, obs, reward, done, info, nullptr, nullptr, 0, nullptr);
+    LaunchArgs<T1, Real> a1 = make_args<T1, Real>(
+        h1, 0, (const char *)actions + n0 * h1->act_stride * R, obs ? (char *)obs + n0 * h1->obs_stride * R : nullptr,
+        reward ? (char *)reward + n0 * R : nullptr, done + n0, info ? (char *)info + n0 * h1->info_stride * R : nullptr,
+        nullptr, nullptr, 0, nullptr);
+    constexpr size_t l0 = lds_bytes<T0, Real, false>(), l1 = lds_bytes<T1, Real, false>();
+    constexpr size_t lds = l0 > l1 ? l0 : l1;
+    static_assert(lds <= 163840, "LDS image + env regions exceed 160 KiB");
+    static bool attr = false;
+    if (!attr) {
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel2<T0, T1, Real>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr = true;
+    }
+    if (a0.blocks + a1.blocks <= 0) return 0;
+    hipLaunchKernelGGL((env_kernel2<T0, T1, Real>), dim3(a0.blocks + a1.blocks), dim3(BIOIM_EPB * T0::G), lds,
+                       h0->stream, a0, a1);
+    return 0;
+}
+
 template <class T, typename Real>
 void id_launch_impl(bioim_handle_t *h, int op, int n, const void *q, const void *u, const void *v, void *out) {
     constexpr int EPB = BIOIM_EPB;
@@ -3720,9 +3768,10 @@ template <class T, typename Real> int upload_smodel(bioim_handle_t *h) {
     return 0;
 }
 
-template <class T> bool pick(const bioim_modelpack_t &p, int precision, Ops &ops) {
+template <class T> bool pick(const bioim_modelpack_t &p, int precision, Ops &ops, const char *name) {
     if (!topology_matches<T>(p)) return false;
     if (p.obs_dim > Lay<T, double>::OBSMAX) return false;
+    ops.topo = name;
     ops.lanes = T::G;
     if (precision == 64) {
         ops.launch = &launch_impl<T, double>;
@@ -3844,9 +3893,29 @@ template <typename Real> int xfer_state(bioim_handle_t *h, double *host, const d
 #define BIOIM_PICK_DECL(S, NAME) bool bioim_pick_##S(const bioim_modelpack_t &p, int precision, Ops &ops);
 BIOIM_FOR_EACH_TOPOLOGY(BIOIM_PICK_DECL)
 #undef BIOIM_PICK_DECL
-#ifndef BIOIM_ABI_ONLY
+/* the fused two-topology launches (the fused unit, or all in this TU):
+ * 1 if (h0, h1) is a pair of BIOIM_FUSED_PAIRS and was launched, 0 if not */
+int bioim_fused_launch(bioim_handle_t *h0, bioim_handle_t *h1, const void *actions, void *obs, void *reward,
+                       uint8_t *done, void *info);
+#if defined(BIOIM_FUSED_ONLY) || (!defined(BIOIM_TOPO_ONLY) && !defined(BIOIM_ABI_ONLY))
+int bioim_fused_launch(bioim_handle_t *h0, bioim_handle_t *h1, const void *actions, void *obs, void *reward,
+                       uint8_t *done, void *info) {
+    /* fp64 only: the fp32 fused kernel of the 3D pair spills 68 B/lane; fp32
+     * batches keep the concurrent per-segment launches */
+    if (h0->precision != 64) return 0;
+#define BIOIM_TRY_PAIR(S0, S1)                                                                      \
+    if (!strcmp(h0->ops.topo, #S0) && !strcmp(h1->ops.topo, #S1)) {                                  \
+        const int rc = fused_launch_impl<S0, S1, double>(h0, h1, actions, obs, reward, done, info);  \
+        return rc ? rc : 1;                                                                          \
+    }
+    BIOIM_FUSED_PAIRS(BIOIM_TRY_PAIR)
+#undef BIOIM_TRY_PAIR
+    return 0;
+}
+#endif
+#if !defined(BIOIM_ABI_ONLY) && !defined(BIOIM_FUSED_ONLY)
 #define BIOIM_PICK_DEF(S, NAME)                                                      \
-    bool bioim_pick_##S(const bioim_modelpack_t &p, int precision, Ops &ops) { return pick<S>(p, precision, ops); }
+    bool bioim_pick_##S(const bioim_modelpack_t &p, int precision, Ops &ops) { return pick<S>(p, precision, ops, #S); }
 #ifdef BIOIM_TOPO_ONLY
 #define BIOIM_PICK_ONE(S, NAME) BIOIM_PICK_DEF(S, NAME)
 BIOIM_TOPOLOGY_AT(BIOIM_TOPO_ONLY, BIOIM_PICK_ONE)
@@ -3857,7 +3926,7 @@ BIOIM_FOR_EACH_TOPOLOGY(BIOIM_PICK_DEF)
 #undef BIOIM_PICK_DEF
 #endif
 
-#ifndef BIOIM_TOPO_ONLY
+#if !defined(BIOIM_TOPO_ONLY) && !defined(BIOIM_FUSED_ONLY)
 thread_local std::string g_err;
 
 /* ================================================================ C-ABI */
@@ -4045,6 +4114,13 @@ int bioim_set_io_strides(bioim_handle_t *h, int act_stride, int obs_stride, int 
     return 0;
 }
 
+static int g_group_fusion = 1;
+
+int bioim_set_group_fusion(int on) {
+    g_group_fusion = on ? 1 : 0;
+    return 0;
+}
+
 int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs, void *reward, uint8_t *done,
                      void *info) {
     if (!hs || nh <= 0 || !actions || !done) return fail(BIOIM_E_ARG, "bioim_step_group: bad arguments");
@@ -4058,14 +4134,23 @@ int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs
     HIPCHK(hipSetDevice(hs[0]->device));
     const size_t R = hs[0]->precision == 64 ? 8 : 4;
     hipStream_t stream = hs[0]->stream;
-    /* One launch per segment, concurrently: segment 0 on the caller's stream
-     * (hs[0]), segment i > 0 on handle i's private stream, forked from and
-     * joined back into the caller's stream with events.  At 4096 envs per GPU
-     * a mixed 50/50 batch gives each segment half the CUs (one 16-env
-     * workgroup per CU); in order on one stream the halves would run one
-     * after the other.  (A fused two-topology kernel — workgroups [0, B0) one
-     * topology, the rest the other — was tried and dropped: its fp64 build
-     * miscompiled the second segment's muscle report) */
+    /* two segments whose topology pair has a fused kernel (BIOIM_FUSED_PAIRS)
+     * and that run the default step kernels (no push table, semi-implicit):
+     * one launch, workgroups [0, B0) segment 0, the rest segment 1 */
+    if (nh == 2 && g_group_fusion && hs[0]->pert_n == 0 && hs[1]->pert_n == 0 && !hs[0]->rk && !hs[1]->rk) {
+        const int rc = bioim_fused_launch(hs[0], hs[1], actions, obs, reward, done, info);
+        if (rc < 0) return rc;
+        if (rc == 1) {
+            HIPCHK(hipGetLastError());
+            return 0;
+        }
+    }
+    /* Otherwise one launch per segment, concurrently: segment 0 on the
+     * caller's stream (hs[0]), segment i > 0 on handle i's private stream,
+     * forked from and joined back into the caller's stream with events.  At
+     * 4096 envs per GPU a mixed 50/50 batch gives each segment half the CUs
+     * (one 16-env workgroup per CU); in order on one stream the halves would
+     * run one after the other. */
     size_t off = 0;
     if (nh > 1) HIPCHK(hipEventRecord(hs[0]->ev_fork, stream));
     for (int i = 0; i < nh; ++i) {

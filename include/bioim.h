@@ -92,13 +92,20 @@ int bioim_set_io_strides(bioim_handle_t *h, int act_stride, int obs_stride, int 
  * device, same precision and strides; auto-reset per handle).  Segment 0 runs
  * on hs[0]'s stream, the others concurrently on private per-handle streams
  * forked from and joined back into it (events), so the call is ordered on
- * hs[0]'s stream like bioim_step.  Later calls on a member handle's own
+ * hs[0]'s stream like bioim_step.  Two segments whose topologies form a fused
+ * pair (the spatial prosthetic and full muscle models, config C5) and that
+ * run the default step (no push table, semi-implicit) go in ONE launch of a
+ * fused two-topology kernel on hs[0]'s stream instead (bioim_set_group_fusion).  Later calls on a member handle's own
  * stream must be ordered after hs[0]'s stream (share one stream, as
  * VectorEnv does).  Replaces nothing in the reference
  * (one OsimModel per Ray worker); the batch is the RLlib VectorEnv over
  * heterogeneous sub-envs. */
 int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs, void *reward, uint8_t *done,
                      void *info);
+/* Process-wide switch of the fused two-topology launch in bioim_step_group
+ * (default on; off: one concurrent launch per segment).  Results are the
+ * same bit for bit either way. */
+int bioim_set_group_fusion(int on);
 /* apply_perturbations (muscle_walking_imitation_env2D.py:83-100 and the same
  * block in every task env): a PrescribedForce on the torso whose ground-frame
  * x force is a PiecewiseConstantFunction of simulation time.  Here: a

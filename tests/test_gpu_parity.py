@@ -242,15 +242,21 @@ def test_sharded_handles_match_unsharded():
 
 
 @pytest.mark.skipif(not gpu_available(), reason='needs GPU')
-@pytest.mark.parametrize('segments', [
-    [('MuscleLockedKneeImitation3D-v0', 40), ('MusclePalsyImitation3D-v0', 56)],
-    [('MuscleWalkingImitation2D-v0', 24), ('MuscleRunningImitation3D-v0', 40), ('TorqueWalkingImitation2D-v0', 8)]])
-def test_mixed_batch_matches_separate_envs(segments):
+@pytest.mark.parametrize('segments,fusion', [
+    ([('MuscleLockedKneeImitation3D-v0', 40), ('MusclePalsyImitation3D-v0', 56)], 1),     # one fused launch
+    ([('MusclePalsyImitation3D-v0', 56), ('MuscleLockedKneeImitation3D-v0', 40)], 1),     # the other pair order
+    ([('MuscleLockedKneeImitation3D-v0', 40), ('MusclePalsyImitation3D-v0', 56)], 0),     # concurrent launches
+    ([('MuscleWalkingImitation2D-v0', 24), ('MuscleRunningImitation3D-v0', 40), ('TorqueWalkingImitation2D-v0', 8)], 1)])
+def test_mixed_batch_matches_separate_envs(segments, fusion):
     """BASELINE config C5: a mixed-topology batch (padded buffers, one
     bioim_step_group call) reproduces each segment stepped on its own, bit
-    for bit, including device-drawn auto-reset rows."""
+    for bit, including device-drawn auto-reset rows — with the fused
+    two-topology kernel (one launch; bioim_set_group_fusion on, the default)
+    and with concurrent per-segment launches."""
     import torch
+    from bioimitation import _lib
     from bioimitation.vector_env import MixedVectorEnv, VectorEnv
+    _lib.load().bioim_set_group_fusion(fusion)
     mixed = MixedVectorEnv(segments, precision=64, seed=21, auto_reset=True)
     alone, off = [], 0
     for env_id, n in segments:
@@ -283,6 +289,7 @@ def test_mixed_batch_matches_separate_envs(segments):
     assert mixed.action_mask.sum().item() == sum(e.num_envs * e.action_dim for e in alone)
     for e in alone + [mixed]:
         e.close()
+    _lib.load().bioim_set_group_fusion(1)
 
 
 @pytest.mark.skipif(not gpu_available(), reason='needs GPU')

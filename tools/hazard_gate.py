@@ -76,7 +76,7 @@ def _scan_unit(obj):
 def scan_build(build_dir: str):
     """[(kernel, instructions, hits)] over every unit, units scanned in parallel"""
     from concurrent.futures import ProcessPoolExecutor
-    objs = sorted(glob.glob(os.path.join(build_dir, 'bioim_topo*.o')))
+    objs = sorted(glob.glob(os.path.join(build_dir, 'bioim_topo*.o')) + glob.glob(os.path.join(build_dir, 'bioim_fused.o')))
     if not objs:
         raise FileNotFoundError(f'no bioim_topo*.o under {build_dir}')
     with ProcessPoolExecutor(min(8, len(objs))) as ex:

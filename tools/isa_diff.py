@@ -24,7 +24,8 @@ def kernels(obj):
 
 def main():
     a, b = sys.argv[1:3]
-    units = sys.argv[3:] or sorted(os.path.basename(f) for f in glob.glob(os.path.join(a, 'bioim_topo*.o')))
+    units = sys.argv[3:] or sorted(os.path.basename(f) for f in glob.glob(os.path.join(a, 'bioim_topo*.o')) +
+                                   glob.glob(os.path.join(a, 'bioim_fused.o')))
     same = diff = 0
     for u in units:
         ka, kb = kernels(os.path.join(a, u)), kernels(os.path.join(b, u))

@@ -13,6 +13,8 @@ for k in $(seq 0 $((NT - 1))); do
   hipcc $FLAGS -DBIOIM_TOPO_ONLY=$k -c --offload-device-only \
       -Rpass-analysis=kernel-resource-usage "$@" -o $tmp/res$k.o bioimitation-gym_amd/csrc/bioim_step.hip > $tmp/res$k.txt 2>&1 &
 done
+hipcc $FLAGS -DBIOIM_FUSED_ONLY -c --offload-device-only \
+    -Rpass-analysis=kernel-resource-usage "$@" -o $tmp/resF.o bioimitation-gym_amd/csrc/bioim_step.hip > $tmp/resF.txt 2>&1 &
 wait
 cat $tmp/res*.txt |
     python3 -c "
