@@ -17,11 +17,19 @@ cp bioimitation-gym_amd/build/libbioim.so.buildid $O/
 if [ "$2" == tests ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
+  if [ -f bioimitation-gym_amd/build/check/libbioim.so ]; then   # the bounds-checked build (BIOIM_CHECK=1)
+    BIOIM_LIB=$PWD/bioimitation-gym_amd/build/check/libbioim.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
+        --timeout 300 --timeout-method thread > $O/gpu_tests_check.log 2>&1
+  fi
 fi
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
 timeout -k 10 300 python bench.py --env-id MuscleRunningImitation3D-v0 --no-cpu-baseline --no-single-env > $O/bench_3d.json 2>> $O/bench.err
 timeout -k 10 300 python bench.py --env-id TorqueWalkingImitation2D-v0 --no-cpu-baseline --no-single-env > $O/bench_torque2d.json 2>> $O/bench.err
 timeout -k 10 300 python bench.py --mixed MuscleLockedKneeImitation3D-v0,MusclePalsyImitation3D-v0 --no-cpu-baseline > $O/bench_mixed.json 2>> $O/bench.err
+timeout -k 10 300 python bench.py --mixed MuscleLockedKneeImitation3D-v0,MusclePalsyImitation3D-v0 --no-cpu-baseline --no-fuse > $O/bench_mixed_nofuse.json 2>> $O/bench.err
+for E in MuscleLockedKneeImitation3D-v0 MusclePalsyImitation3D-v0; do
+  timeout -k 10 300 python bench.py --env-id $E --no-cpu-baseline --no-single-env --no-reference-integrator > $O/bench_$E.json 2>> $O/bench.err
+done
 for CFG in "2d:MuscleWalkingImitation2D-v0" "3d:MuscleRunningImitation3D-v0"; do
     K=${CFG%%:*}; E=${CFG#*:}
     A="--env-id $E --steps 20 --warmup 3 --no-cpu-baseline --no-reference-integrator --no-single-env"
