@@ -15,7 +15,7 @@ mkdir -p $O
 export TMPDIR=/tmp
 cp bioimitation-gym_amd/build/libbioim.so.buildid $O/
 if [ "$2" == tests ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
   if [ -f bioimitation-gym_amd/build/check/libbioim.so ]; then   # the bounds-checked build (BIOIM_CHECK=1)
     BIOIM_LIB=$PWD/bioimitation-gym_amd/build/check/libbioim.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
