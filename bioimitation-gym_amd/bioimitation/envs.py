@@ -128,10 +128,12 @@ class ImitationEnv:
             self._names = load_names(self.env_id)
         return obs_to_dict(o, self._env.pack, self._names)
 
-    def _record_row(self, o, stepped=True):
-        """o: the env's observation row on the host"""
+    def _record_row(self, o, stepped=True, fr=None):
+        """o: the env's observation row on the host; fr: its force-report row
+        when the caller has already copied it"""
         if self._record:
-            fr = self._env.force_report[0].double().cpu().numpy()
+            if fr is None:
+                fr = self._env.force_report[0].double().cpu().numpy()
             self.osim_model.record_row(self._env.get_state()[0], o[self._qdd], fr, stepped)
 
     def reset(self, obs_as_dict=False):
@@ -150,13 +152,17 @@ class ImitationEnv:
                             device=self._env.device)
         obs, rew, done, info = self._env.step(a)
         self.osim_model._dirty()
-        # one device-to-host copy for the step's outputs (each .cpu() waits on the stream)
-        out = torch.cat([obs[0], rew[:1], info[0], done[:1].to(obs.dtype)]).double().cpu().numpy()
+        # one device-to-host copy for the step's outputs (each .cpu() waits on the stream),
+        # the force-report row included when recording
+        parts = [obs[0], rew[:1], info[0], done[:1].to(obs.dtype)]
+        if self._record:
+            parts.append(self._env.force_report[0])
+        out = torch.cat(parts).double().cpu().numpy()
         nobs, ninf = obs.shape[1], info.shape[1]
         o = out[:nobs]
-        self._record_row(o)
+        self._record_row(o, fr=out[nobs + 1 + ninf + 1:] if self._record else None)
         inf = [float(v) for v in out[nobs + 1:nobs + 1 + ninf]]
-        self._last = (float(out[nobs]), inf, bool(out[-1]))
+        self._last = (float(out[nobs]), inf, bool(out[nobs + 1 + ninf]))
         return [self._out(o[None, :], obs_as_dict), self._last[0], self._last[2], {'all_rewards': inf}]
 
     # -- the task envs' public methods (muscle_walking_imitation_env2D.py:102-403,
