@@ -49,9 +49,12 @@ def _worker(rank, world, port, total, q):
     dist.init_process_group('gloo', rank=rank, world_size=world)
     lo, hi = shard_range(total, rank, world)
     mine = torch.from_numpy(_rollout(lo, hi))
-    parts = [torch.zeros((shard_range(total, r, world)[1] - shard_range(total, r, world)[0],) + tuple(mine.shape[1:]),
-                         dtype=mine.dtype) for r in range(world)]
-    dist.all_gather(parts, mine)
+    sizes = [shard_range(total, r, world)[1] - shard_range(total, r, world)[0] for r in range(world)]
+    pad = torch.zeros((max(sizes),) + tuple(mine.shape[1:]), dtype=mine.dtype)   # gloo gathers equal shapes
+    pad[:len(mine)] = mine
+    parts = [torch.zeros_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    parts = [p_[:k] for p_, k in zip(parts, sizes)]
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     if rank == 0:
@@ -60,14 +63,18 @@ def _worker(rank, world, port, total, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_gloo_sharding_is_bit_identical():
+@pytest.mark.parametrize('world', [2, 4])
+def test_gloo_sharding_is_bit_identical(world):
+    """world ranks (2, and 4 to rehearse more than two), uneven shards of 10
+    envs: the gathered shards equal the unsharded rollout bit for bit, and
+    the max-over-ranks reduction bench.py times with sees every rank"""
     total = 10
     with socket.socket() as s:
         s.bind(('127.0.0.1', 0))
         port = s.getsockname()[1]
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, total, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, total, q)) for r in range(world)]
     for p in ps:
         p.start()
     gathered, tmax = q.get(timeout=120)
@@ -76,7 +83,7 @@ def test_two_rank_gloo_sharding_is_bit_identical():
         assert p.exitcode == 0
     single = _rollout(0, total)
     np.testing.assert_array_equal(gathered, single)
-    assert tmax == 2.0
+    assert tmax == float(world)
 
 
 def test_bench_refuses_mismatched_world_size():
