@@ -201,3 +201,50 @@ def test_ik_frames_body_positions_on_hip_path(tag):
     print(f'{tag}: {n} IK frames, {len(cols)} body-position / coordinate columns, HIP vs oracle max rel err {worst:.2e}')
     assert worst < 1e-12
     env.close()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+def test_c4_whole_node_batch_on_one_gpu_vs_oracle():
+    """Maximum size: config C4's whole-node batch (32768 envs of
+    MuscleRunningImitation3D-v0, 2048 workgroups: eight passes over the CUs)
+    on ONE GPU, with auto-reset, 6 steps — index arithmetic past 2^15 envs,
+    the last workgroup, the device reset draws keyed by a global index beyond
+    any single shard's.  A strided sample (the first and last workgroup, envs
+    around every 4096 boundary) matches the oracle to 1e-6 (observed at the
+    rounding level as in the 4096-env test above)."""
+    import torch
+    import oracle
+    from bioimitation.registry import load_pack
+    from bioimitation.vector_env import VectorEnv
+    env_id, n, T = 'MuscleRunningImitation3D-v0', 32768, 6
+    pk = load_pack(env_id)
+    env = VectorEnv(env_id, n, precision=64, seed=9, auto_reset=False)
+    epw = env.launch['envs_per_workgroup']
+    assert env.launch['workgroups'] == n // epw == 2048
+    rng = np.random.default_rng(45)
+    rows = rng.integers(0, pk.reset_hi + 1, size=n)
+    env.reset(ref_index=rows)
+    bounds = np.arange(4096, n, 4096)
+    check = np.unique(np.concatenate([np.arange(epw), np.arange(n - epw, n), bounds - 1, bounds,
+                                      np.arange(0, n, 997)]))
+    orc = oracle.Oracle(pk)
+    bufs = orc.new_envs(len(check))
+    for j, i in enumerate(check):
+        orc.reset(bufs, j, int(rows[i]))
+    alive = np.ones(len(check), bool)
+    worst = 0.0
+    for t in range(T):
+        acts = rng.uniform(0.0, 1.0, size=(n, pk.nact))
+        obs, rew, done, info = (x.cpu().numpy() for x in env.step(torch.as_tensor(acts, device=env.device)))
+        assert np.isfinite(obs).all()
+        for j, i in enumerate(check):
+            if not alive[j]:
+                continue
+            o, r, d, inf = orc.step(bufs, j, acts[i])
+            e = max(_rel(obs[i], o).max(), abs(rew[i] - r), _rel(info[i], inf).max())
+            assert e < 1e-6, (t, i, e)
+            assert bool(done[i]) == d, (t, i)
+            worst = max(worst, e)
+            alive[j] = not d
+    print(f'{env_id} {n} envs on one GPU x {T} steps: {len(check)} envs checked, max rel err {worst:.2e}')
+    env.close()
