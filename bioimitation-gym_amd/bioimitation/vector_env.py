@@ -254,6 +254,8 @@ class VectorEnv:
         if env_ids is not None:
             ids = self._env_ids(env_ids)
             n = ids.numel()
+            if n == 0:          # nothing listed: nothing to reset (a null id list would mean every env)
+                return self.obs
         if ref_index is not None:
             rows = torch.as_tensor(ref_index, dtype=torch.int32, device=self.device).contiguous()
             if ids is None:

@@ -357,3 +357,24 @@ def test_rk_analyses_record_every_integration_step(tmp_path):
     for key in ('states', 'q', 'u', 'dudt', 'forces'):
         assert len(read_sto(paths[key])[2]) == 1 + len(want_qdd), key
     env.close()
+
+
+def test_empty_and_duplicate_env_lists():
+    """Edge cases of the listed-env calls: an empty list resets / realizes
+    nothing (the state is unchanged bit for bit), a repeated or out-of-range
+    id is refused before any launch (two lane groups would race on one env's
+    state; VectorEnv._env_ids)."""
+    from bioimitation.vector_env import VectorEnv
+    env = VectorEnv('MuscleWalkingImitation2D-v0', 20, precision=64, seed=3)
+    env.reset()
+    before = env.get_state()
+    env.reset(env_ids=[], ref_index=[])
+    env.osim('realize', [])
+    np.testing.assert_array_equal(env.get_state(), before)
+    for bad in ([1, 1], [0, 20], [-1]):
+        with pytest.raises(ValueError):
+            env.osim('realize', bad)
+        with pytest.raises(ValueError):
+            env.reset(env_ids=bad)
+    np.testing.assert_array_equal(env.get_state(), before)
+    env.close()
