@@ -209,6 +209,9 @@ def main():
                          "MuscleLockedKneeImitation3D-v0,MusclePalsyImitation3D-v0")
     ap.add_argument('--no-fuse', action='store_true',
                     help='mixed batch: concurrent per-segment launches instead of the fused two-topology kernel')
+    ap.add_argument('--share-gpu', action='store_true',
+                    help='REHEARSAL ONLY: let ranks share the visible GPU(s) (rank r on GPU r mod count) to run '
+                         'the multi-rank path on a 1-GPU box; the line is marked "rehearsal" and is no scaling number')
     a = ap.parse_args()
     if a.rk_budget and (a.integrator != 'rk-merson' or a.mixed):
         ap.error('--rk-budget needs --integrator rk-merson and a single env id')
@@ -226,8 +229,11 @@ def main():
     import numpy as np
     import torch
     if local >= torch.cuda.device_count():
-        print(f'bench.py: rank {rank} needs GPU {local} but {torch.cuda.device_count()} are visible', file=sys.stderr)
-        sys.exit(2)
+        if not a.share_gpu:
+            print(f'bench.py: rank {rank} needs GPU {local} but {torch.cuda.device_count()} are visible',
+                  file=sys.stderr)
+            sys.exit(2)
+        local %= torch.cuda.device_count()
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -338,6 +344,8 @@ def main():
             'burn_in': a.burn_in, 'ms_per_step': t_max / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': f'f{a.precision}', 'done_rate': done_rate, 'build_id': build_id,
             'data': 'synthetic: PCG64 U[0,1] muscle excitations; reference motion synthesized from the shipped 3D IK',
+            **({'rehearsal': f'{world} ranks shared {torch.cuda.device_count()} GPU(s) (--share-gpu): the multi-rank '
+                              'code path, not a scaling number'} if a.share_gpu else {}),
             'config': {'workload': f'{a.env_id} batched env.step, {n} envs/GPU, ' +
                        (f'nsub={env.nsub}' if a.integrator == 'semi-implicit' else 'RK-Merson 1e-3') + ', auto-reset',
                        'integrator': a.integrator, 'rk_budget': a.rk_budget or None,
