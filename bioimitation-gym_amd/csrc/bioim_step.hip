@@ -3714,11 +3714,14 @@ int fused_launch_impl(bioim_handle_t *h0, bioim_handle_t *h1, const void *action
     constexpr size_t l0 = lds_bytes<T0, Real, false>(), l1 = lds_bytes<T1, Real, false>();
     constexpr size_t lds = l0 > l1 ? l0 : l1;
     static_assert(lds <= 163840, "LDS image + env regions exceed 160 KiB");
-    static bool attr = false;
-    if (!attr) {
+    /* the dynamic-LDS attribute is per device: set it once on each (the
+     * per-topology kernels set theirs at handle creation, upload_smodel) */
+    static bool attr[64] = {};
+    const int dev = h0->device;
+    if (dev < 0 || dev >= 64 || !attr[dev]) {
         HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&env_kernel2<T0, T1, Real>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr = true;
+        if (dev >= 0 && dev < 64) attr[dev] = true;
     }
     if (a0.blocks + a1.blocks <= 0) return 0;
     hipLaunchKernelGGL((env_kernel2<T0, T1, Real>), dim3(a0.blocks + a1.blocks), dim3(BIOIM_EPB * T0::G), lds,
