@@ -253,10 +253,17 @@ def test_mixed_batch_matches_separate_envs(segments, fusion):
     for bit, including device-drawn auto-reset rows — with the fused
     two-topology kernel (one launch; bioim_set_group_fusion on, the default)
     and with concurrent per-segment launches."""
-    import torch
     from bioimitation import _lib
-    from bioimitation.vector_env import MixedVectorEnv, VectorEnv
     _lib.load().bioim_set_group_fusion(fusion)
+    try:
+        _mixed_batch_check(segments)
+    finally:
+        _lib.load().bioim_set_group_fusion(1)      # the process-wide default
+
+
+def _mixed_batch_check(segments):
+    import torch
+    from bioimitation.vector_env import MixedVectorEnv, VectorEnv
     mixed = MixedVectorEnv(segments, precision=64, seed=21, auto_reset=True)
     alone, off = [], 0
     for env_id, n in segments:
@@ -289,7 +296,6 @@ def test_mixed_batch_matches_separate_envs(segments, fusion):
     assert mixed.action_mask.sum().item() == sum(e.num_envs * e.action_dim for e in alone)
     for e in alone + [mixed]:
         e.close()
-    _lib.load().bioim_set_group_fusion(1)
 
 
 @pytest.mark.skipif(not gpu_available(), reason='needs GPU')
