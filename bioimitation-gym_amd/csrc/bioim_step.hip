@@ -2349,17 +2349,36 @@ DEV void osim_report(const DModel<Real> &M, const SModel<T, Real> &SM, const Rea
     constexpr int OLIM = OCF + 6 * T::NF, OCOT = OLIM + T::NL;
     const Real x0 = D.x0;
     if (lane == 0) { out[0] = Real(t); out[1] = Real(istep); }
+    /* the muscle rows first: their fiber states then die before the body
+     * terms below are live (3D REP kernels: fewer values spilled) */
+    Real cot = 0;
+#pragma unroll
+    for (int j = 0; j < MPL; ++j) {
+        const int m = mslot<T>(lane + j * G);
+        if constexpr (NM > 0) {
+            if (m < NM) {
+                const MState<Real> &ms = D.ms[j];
+                Real *o = out + OMU + 7 * m;
+                o[0] = ms.act; o[1] = ms.lce; o[2] = ms.vce; o[3] = ms.Ff; o[4] = ms.Fa; o[5] = control[j]; o[6] = ms.Ft;
+                cot += muscle_cot<Real>(SM.mus[m], ms, control[j]);
+            }
+        }
+        if (m < NA) {
+            if constexpr (NM > 0) out[OACT + m] = D.ms[j].Ft;
+            else out[OACT + m] = control[j] * SM.ca_opt[m];
+        }
+    }
+    cot = group_sum<G>(cot);
+    if (lane == 0) out[OCOT] = NM > 0 ? cot + Real(1.51) * M.total_mass : Real(0);
     /* loops over bodies, spheres and coordinates run rolled (unroll 1): the
      * report is off the stepping path, and unrolled it held every body's terms
      * live at the kernel's peak register pressure — 0.6-2.9 KB/lane of scratch
-     * in the REP kernels before (profiles/r03/resources.txt).  Except in the
-     * spatial prosthetic muscle model (5 composite bodies, 19 muscles): rolled,
-     * its non-RK REP kernels got two lane-divergent AGPR copies of the env
-     * offset that tools/hazard_gate.py flags, so it keeps the
-     * unrolled loops and their scratch */
-    constexpr int UC = (T::PLANAR || T::NB >= 7 || NM == 0) ? 1 : CPL;
-    constexpr int UB = (T::PLANAR || T::NB >= 7 || NM == 0) ? 1 : T::NB;
-    constexpr int US = (T::PLANAR || T::NB >= 7 || NM == 0) ? 1 : T::NS;
+     * in the REP kernels (profiles/r03/resources.txt).  (Round 4's first cut
+     * kept the prosthetic model's loops unrolled: rolled, its non-RK REP
+     * kernels then got two lane-divergent AGPR copies of the env offset that
+     * tools/hazard_gate.py flags; with the compile-time mode of the REP
+     * kernels (env_block) the rolled form is clean there too.) */
+    constexpr int UC = 1, UB = 1, US = 1;
 #pragma unroll UC
     for (int jc = 0; jc < CPL; ++jc) {
         const int c = lane + jc * G;
@@ -2386,29 +2405,33 @@ DEV void osim_report(const DModel<Real> &M, const SModel<T, Real> &SM, const Rea
         }
     };
     if (lane < NOS) {
+        /* each term stored as soon as it is computed (fewer values live at once) */
         const int cb = SM.os_cb[lane];
         const Real *kb = lds + LY::KB + 18 * cb;
-        Real P[3], v[3], tt[3], al[3], aO[3], aP[3], Rb[9], ang[3];
+        Real *o = out + OB + 18 * lane;
+        {
+            Real Rb[9], ang[3];
+            mm3(kb, M.os_R[lane], Rb);
+            body_fixed_xyz(Rb, ang);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { o[9 + i] = ang[i]; o[12 + i] = kb[12 + i]; }
+        }
+        Real P[3], v[3], tt[3], al[3], aO[3];
         mv3(kb, SM.os_p[lane], P);
 #pragma unroll
         for (int i = 0; i < 3; ++i) P[i] += kb[9 + i];
         cross3(kb + 12, P, tt);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) v[i] = kb[15 + i] + tt[i];
+        for (int i = 0; i < 3; ++i) {
+            v[i] = kb[15 + i] + tt[i];
+            o[i] = P[i] + (i == 0 ? x0 : Real(0)); o[3 + i] = v[i];
+        }
         body_acc(cb, al, aO);
         Real t2[3];
         cross3(al, P, tt);
         cross3(kb + 12, v, t2);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) aP[i] = aO[i] + tt[i] + t2[i];
-        mm3(kb, M.os_R[lane], Rb);
-        body_fixed_xyz(Rb, ang);
-        Real *o = out + OB + 18 * lane;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            o[i] = P[i] + (i == 0 ? x0 : Real(0)); o[3 + i] = v[i]; o[6 + i] = aP[i];
-            o[9 + i] = ang[i]; o[12 + i] = kb[12 + i]; o[15 + i] = al[i];
-        }
+        for (int i = 0; i < 3; ++i) { o[6 + i] = aO[i] + tt[i] + t2[i]; o[15 + i] = al[i]; }
     } else if (lane == NOS) {
         Real mt = 0, cs[3] = {0, 0, 0}, vs[3] = {0, 0, 0}, as[3] = {0, 0, 0};
 #pragma unroll UB
@@ -2437,23 +2460,6 @@ DEV void osim_report(const DModel<Real> &M, const SModel<T, Real> &SM, const Rea
             o[i] = cs[i] / mt + (i == 0 ? x0 : Real(0)); o[3 + i] = vs[i] / mt; o[6 + i] = as[i] / mt;
         }
     }
-    Real cot = 0;
-#pragma unroll
-    for (int j = 0; j < MPL; ++j) {
-        const int m = mslot<T>(lane + j * G);
-        if constexpr (NM > 0) {
-            if (m < NM) {
-                const MState<Real> &ms = D.ms[j];
-                Real *o = out + OMU + 7 * m;
-                o[0] = ms.act; o[1] = ms.lce; o[2] = ms.vce; o[3] = ms.Ff; o[4] = ms.Fa; o[5] = control[j]; o[6] = ms.Ft;
-                cot += muscle_cot<Real>(SM.mus[m], ms, control[j]);
-            }
-        }
-        if (m < NA) {
-            if constexpr (NM > 0) out[OACT + m] = D.ms[j].Ft;
-            else out[OACT + m] = control[j] * SM.ca_opt[m];
-        }
-    }
     if (lane < T::NF) {
         Real F[3] = {0, 0, 0}, Mo[3] = {0, 0, 0};
 #pragma unroll US
@@ -2469,8 +2475,6 @@ DEV void osim_report(const DModel<Real> &M, const SModel<T, Real> &SM, const Rea
         for (int i = 0; i < 3; ++i) { out[OCF + 6 * lane + i] = F[i]; out[OCF + 6 * lane + 3 + i] = Mo[i]; }
     }
     if (lane < T::NL) out[OLIM + lane] = lds[LY::LIM + 4 * lane];
-    cot = group_sum<G>(cot);
-    if (lane == 0) out[OCOT] = NM > 0 ? cot + Real(1.51) * M.total_mass : Real(0);
 }
 
 /* One 256-thread workgroup = 256/G envs of segment `a`, block `blk`.
@@ -2485,9 +2489,12 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const DModel<Real> *__restrict__ Mg = a.Mg;
     const DState<Real> &st = a.st;
-    const int N = a.N, mode = a.mode;
-    /* mode 2 (OsimModel calls) exists in the REP kernels only */
-    const bool osim = REP && mode == 2;
+    /* mode 2 (OsimModel calls) exists in the REP kernels only, and they run
+     * nothing else (launch_impl): a compile-time mode there, so the step's
+     * reward / termination / auto-reset tail and the RK carry past the report
+     * are dead code in them instead of live registers */
+    const int N = a.N, mode = REP ? 2 : a.mode;
+    const bool osim = REP;
     const Real *__restrict__ actions = a.actions;
     Real *__restrict__ obs = a.obs;
 #ifdef BIOIM_STAMPS
@@ -2530,8 +2537,12 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     Real qd = 0, ud = 0;
     if (lane < ND) { qd = GAT(st.q, (size_t)lane * N + env, (size_t)ND * N); ud = GAT(st.u, (size_t)lane * N + env, (size_t)ND * N); }
     double t = GAT(st.t, env, (size_t)N);
-    int istep = GAT(st.istep, env, (size_t)N), has_last = GAT(st.has_last, env, (size_t)N), resets = GAT(st.resets, env, (size_t)N);
-    Real old_px = GAT(st.old_px, env, (size_t)N);
+    /* has_last, resets, old_px and last[] change only in a step (mode 0) or a
+     * reset (mode 1): the REP kernels neither load nor store them, instead of
+     * carrying them through the kernel unchanged */
+    int istep = GAT(st.istep, env, (size_t)N), has_last = REP ? 0 : GAT(st.has_last, env, (size_t)N),
+        resets = REP ? 0 : GAT(st.resets, env, (size_t)N);
+    Real old_px = REP ? Real(0) : GAT(st.old_px, env, (size_t)N);
     Real act[MPL], lce[MPL], control[MPL], curr[MPL], last[MPL], hist[MPL][BIOIM_MAX_HORIZON];
 #pragma unroll
     for (int j = 0; j < MPL; ++j) {
@@ -2541,7 +2552,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
 #pragma unroll
         for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh) hist[j][hh] = 0;
         if (m < NA) {
-            last[j] = GAT(st.last, (size_t)m * N + env, (size_t)NA * N);
+            if (!REP) last[j] = GAT(st.last, (size_t)m * N + env, (size_t)NA * N);
 #pragma unroll
             for (int hh = 0; hh < BIOIM_MAX_HORIZON; ++hh)
                 hist[j][hh] = hh < H ? GAT(st.hist, ((size_t)hh * NA + m) * N + env, (size_t)BIOIM_MAX_HORIZON * NA * N) : Real(0);
@@ -2553,7 +2564,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     Real rew = 0, inf[5] = {0, 0, 0, 0, 0};
     bool do_reset = (mode == 1);
     /* budgeted RK: a suspended step resumes (its action row is ignored) */
-    const bool budget = RK && a.rk_budget > 0;
+    const bool budget = RK && !REP && a.rk_budget > 0;   /* make_args: 0 unless mode 0 */
     const bool resume = RK && mode == 0 && GAT(st.pend, env, (size_t)N) != 0;
     bool suspend = false;
     /* RK: dynamics evaluations spent in this launch (the budget is 5 per
@@ -2999,8 +3010,15 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             }
         }
         if constexpr (REP) {
-            if (osim && a.osim_out)
+            /* the observation rows first, so the report runs with ob's
+             * addresses dead (the spatial push + RK report kernel is at 512) */
+            wave_sync();
+            if (obs)
+                for (int k = lane; k < M.obs_dim; k += G) GAT(obs, (size_t)env * a.obs_stride + k, (size_t)N * a.obs_stride) = ob[k];
+            wave_sync();
+            if (a.osim_out)
                 osim_report<T, Real>(M, SM, lds, lane, D, control, t, istep, a.osim_out + GIDX((size_t)env, (size_t)N) * a.osim_dim);
+            break;
         }
         wave_sync();
         if (obs)
@@ -3124,10 +3142,12 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         if (lane == 0) {
         GAT(st.t, env, (size_t)N) = t;
         GAT(st.istep, env, (size_t)N) = istep;
-        GAT(st.has_last, env, (size_t)N) = has_last;
-        GAT(st.old_px, env, (size_t)N) = old_px;
-        if (!osim) GAT(st.done, env, (size_t)N) = (mode == 0 && !do_reset && !suspend) ? done : 0;
-        GAT(st.resets, env, (size_t)N) = resets;
+        if (!REP) {
+            GAT(st.has_last, env, (size_t)N) = has_last;
+            GAT(st.old_px, env, (size_t)N) = old_px;
+            GAT(st.done, env, (size_t)N) = (mode == 0 && !do_reset && !suspend) ? done : 0;
+            GAT(st.resets, env, (size_t)N) = resets;
+        }
         if (RK || mode == 1 || (osim && a.osim_op == BIOIM_OSIM_EQUILIBRATE)) GAT(st.hrk, env, (size_t)N) = rk_hnext;
         if constexpr (RK) {
             GAT(st.pend, env, (size_t)N) = suspend ? 1 : 0;
@@ -3157,9 +3177,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     for (int j = 0; j < MPL; ++j) {
         const int m = mslot<T>(lane + j * G);
         if (NM > 0 && m < NM) { GAT(st.act, (size_t)m * N + env, (size_t)(NM > 0 ? NM : 1) * N) = act[j]; GAT(st.lce, (size_t)m * N + env, (size_t)(NM > 0 ? NM : 1) * N) = lce[j]; }
-        if (m < NA) {
-            GAT(st.last, (size_t)m * N + env, (size_t)NA * N) = last[j];
-        }
+        if (!REP && m < NA) GAT(st.last, (size_t)m * N + env, (size_t)NA * N) = last[j];
     }
 }
 

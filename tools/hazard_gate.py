@@ -10,7 +10,7 @@ read uses as a memory address ("masked-use+addr") or that no lane wrote
     python tools/hazard_gate.py [build-dir] --baseline   # record the per-kernel counts (profiles/r04)
 
 The scan is conservative (it cannot tell that a later region selects a subset
-of the copy's lanes); the shipped build carries none in any of its 126
+of the copy's lanes); the shipped build carries none in any of its 128
 kernels, and tests/test_hazard_gate.py requires exactly that.
 """
 from __future__ import annotations
@@ -81,6 +81,44 @@ def scan_build(build_dir: str):
         raise FileNotFoundError(f'no bioim_topo*.o under {build_dir}')
     with ProcessPoolExecutor(min(8, len(objs))) as ex:
         return [k for unit in ex.map(_scan_unit, objs) for k in unit]
+
+
+def _unit_resources(obj):
+    """{kernel: (scratch bytes/lane, registers, AGPRs)} from the code object's
+    metadata notes (.private_segment_fixed_size; .vgpr_count, which on gfx950
+    is the unified VGPR + AGPR allocation; .agpr_count)"""
+    out, cur = {}, {}
+    with tempfile.TemporaryDirectory() as tmp:
+        disassemble(obj, tmp)   # leaves the unbundled code object in tmp
+        co = os.path.join(tmp, os.path.basename(obj) + '.co')
+        notes = subprocess.run([os.path.join(LLVM, 'llvm-readelf'), '--notes', co],
+                               check=True, capture_output=True, text=True).stdout
+    for ln in notes.split('\n'):
+        m = re.match(r'\s*(?:- )?\.(name|private_segment_fixed_size|vgpr_count|agpr_count):\s+(\S+)', ln)
+        if not m:
+            continue
+        if ln.lstrip().startswith('- '):   # a new kernel record
+            cur = {}
+        cur[m.group(1)] = m.group(2)
+        if {'name', 'private_segment_fixed_size', 'vgpr_count', 'agpr_count'} <= cur.keys():
+            n = cur['name']
+            if 'env_kernel' in n or 'id_kernel' in n:
+                out[n] = (int(cur['private_segment_fixed_size']), int(cur['vgpr_count']), int(cur['agpr_count']))
+            cur = {}
+    return out
+
+
+def resources(build_dir: str) -> dict:
+    """{kernel: (scratch bytes/lane, registers, AGPRs)} over every unit of a build"""
+    from concurrent.futures import ProcessPoolExecutor
+    objs = sorted(glob.glob(os.path.join(build_dir, 'bioim_topo*.o')) + glob.glob(os.path.join(build_dir, 'bioim_fused.o')))
+    if not objs:
+        raise FileNotFoundError(f'no bioim_topo*.o under {build_dir}')
+    res = {}
+    with ProcessPoolExecutor(min(8, len(objs))) as ex:
+        for unit in ex.map(_unit_resources, objs):
+            res.update(unit)
+    return res
 
 
 def per_kernel(build_dir: str) -> dict:
