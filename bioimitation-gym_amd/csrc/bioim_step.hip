@@ -526,7 +526,7 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
         i0 = i0 < 0 ? 0 : (i0 > BIOIM_UTAB - 1 ? BIOIM_UTAB - 1 : i0);
         Real fr = tt - Real(i0);
         const Real ua = C.ut[k][i0], ub = C.ut[k][i0 + 1];
-        const Real ut = ua + fr * (ub - ua), us = ga / (ga - gb);
+        const Real ut = ua + fr * (ub - ua), us = ga * newton_rcp(ga - gb);
         u = ((v0 > xa) & (v0 < xb)) ? ut : us;
     }
     const Real half = 0.5;
@@ -571,11 +571,15 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
             v = (rhs - afal * (C.y1 - C.dydx1 * C.x1)) / (afal * C.dydx1 + beta);
             fv = C.y1 + C.dydx1 * (v - C.x1); dfv = C.dydx1;
         }
-    } else {   /* linear extrapolation past an end (one division, selected) */
+    } else {   /* linear extrapolation past an end (one reciprocal, selected).
+                * Reciprocals instead of IEEE divisions here and in the secant
+                * start: same-box 2D 0.2772 -> 0.2762 ms, 3D 0.5176 -> 0.5145 ms,
+                * C5 unchanged (profiles/r04/r04y; computing this before the
+                * Newton loop instead was 2D -0.6 % but C5 +1.2 %) */
         const Real y0 = C.y0, d0 = C.dydx0, x0 = C.x0, y1 = C.y1, d1 = C.dydx1, x1 = C.x1;
         const bool e0 = g0 >= 0, e1 = g1 <= 0;
         const Real yE = e0 ? y0 : y1, dE = e0 ? d0 : d1, xE = e0 ? x0 : x1;
-        const Real vE = (rhs - afal * (yE - dE * xE)) / (afal * dE + beta);
+        const Real vE = (rhs - afal * (yE - dE * xE)) * fast_rcp(afal * dE + beta);
         const Real fvE = yE + dE * (vE - xE);
         const bool ext = e0 | e1;
         v = ext ? vE : v; fv = ext ? fvE : fv; dfv = ext ? dE : dfv;
