@@ -365,7 +365,7 @@ def main():
         if world == 1 and not a.mixed and not a.no_single_env:
             line['single_env'] = single_env_rate()
     env.close()
-    if not (a.no_reference_integrator or a.mixed or a.integrator != 'semi-implicit'):
+    if not (a.no_reference_integrator or a.integrator != 'semi-implicit'):
         ref = reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist)
         if rank == 0:
             line['reference_integrator'] = ref
@@ -383,23 +383,44 @@ def reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist):
     reference's integrator: RK-Merson at accuracy 1e-3 in budgeted launches
     (bioim_set_rk_budget; trajectories identical to unbudgeted RK).  Burned in
     by finished env steps to the same horizon as the main measurement; value =
-    env steps finished in a.steps timed launches over all ranks / max time."""
+    env steps finished in a.steps timed launches over all ranks / max time.
+    A mixed batch (C5) runs as a MixedVectorEnv whose segments each carry
+    their own budget and ready rows (concurrent per-segment launches: the
+    fused kernel is semi-implicit only)."""
     import torch
-    from bioimitation.vector_env import VectorEnv
+    from bioimitation.vector_env import MixedVectorEnv, VectorEnv
     n = a.envs
-    env = VectorEnv(a.env_id, n, config={'integrator': 'rk-merson'}, device=dev.index, precision=a.precision,
-                    seed=1000, auto_reset=True, env_offset=rank * n)
-    env.set_rk_budget(RK_BUDGET)
+    if a.mixed:
+        ids = a.mixed.split(',')
+        sizes = [n // len(ids)] * len(ids)
+        sizes[-1] += n - sum(sizes)
+        env = MixedVectorEnv(list(zip(ids, sizes)), config={'integrator': 'rk-merson'}, device=dev.index,
+                             precision=a.precision, seed=1000, auto_reset=True, env_offset=rank * n)
+        segs = env.envs
+    else:
+        env = VectorEnv(a.env_id, n, config={'integrator': 'rk-merson'}, device=dev.index, precision=a.precision,
+                        seed=1000, auto_reset=True, env_offset=rank * n)
+        segs = [env]
+    for e in segs:
+        e.set_rk_budget(RK_BUDGET)
     env.reset()
     fin = torch.zeros(n, dtype=torch.int32, device=dev)
+    fins, off = [], 0
+    for e in segs:   # each segment's rows of fin
+        fins.append(fin[off:off + e.num_envs])
+        off += e.num_envs
+
+    def count_ready():
+        for f, e in zip(fins, segs):
+            f += e.ready
     k0 = 0
     while k0 < 50 * (a.burn_in + a.warmup) and (k0 % 10 or int(fin.sum()) < n * (a.burn_in + a.warmup)):
         env.step(acts[k0 % pool])
-        fin += env.ready
+        count_ready()
         k0 += 1
-    resets0 = env.reset_count()
-    counted = hasattr(env._L, 'bioim_eval_count')    # older A/B builds lack the counter
-    evals0 = env.eval_count() if counted else 0
+    resets0 = sum(e.reset_count() for e in segs)
+    counted = hasattr(segs[0]._L, 'bioim_eval_count')    # older A/B builds lack the counter
+    evals0 = sum(e.eval_count() for e in segs) if counted else 0
     fin.zero_()
     if dist:
         dist.barrier()
@@ -407,7 +428,7 @@ def reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist):
     t0 = time.perf_counter()
     for k in range(a.steps):
         env.step(acts[(k0 + k) % pool])
-        fin += env.ready
+        count_ready()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     if dist:
@@ -423,8 +444,8 @@ def reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist):
         tot = float(st_[0])
     rate = {'value': tot / t_max, 'unit': 'finished env-steps/s', 'integrator': 'rk-merson', 'accuracy': 1e-3,
             'rk_budget': RK_BUDGET, 'launches': a.steps, 'ms_per_launch': t_max / a.steps * 1e3,
-            'finished_env_steps': tot, 'done_rate': (env.reset_count() - resets0) / max(local, 1),
-            'evals_per_env_step': (env.eval_count() - evals0) / max(local, 1) if counted else None,
+            'finished_env_steps': tot, 'done_rate': (sum(e.reset_count() for e in segs) - resets0) / max(local, 1),
+            'evals_per_env_step': (sum(e.eval_count() for e in segs) - evals0) / max(local, 1) if counted else None,
             'note': "the reference's integrator (opensim_wrapper.py:287-301) on the same workload; "
                     'GPU parity vs the oracle in tests/test_gpu_parity.py (RK) and tests/test_gpu_rk_budget.py'}
     env.close()

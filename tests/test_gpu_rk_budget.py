@@ -160,3 +160,43 @@ def test_rllib_base_env_async_equals_sync(integrator, env_id):
     print(f'{env_id} ({integrator}): {rounds} rounds for {T} steps per env')
     assert (k >= T).all(), k
     benv.stop()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs a HIP GPU')
+def test_mixed_batch_rk_budget_matches_segments_alone():
+    """BASELINE config C5 with the reference's integrator in budgeted launches
+    (bench.py's reference_integrator leg for --mixed): each segment of a
+    MixedVectorEnv carries its own budget and ready rows, and every launch's
+    obs / reward / done / ready rows equal the segment stepped alone with the
+    same budget, bit for bit, through auto-resets."""
+    import torch
+    from bioimitation.vector_env import MixedVectorEnv, VectorEnv
+    segments = [('MuscleLockedKneeImitation3D-v0', 24), ('MusclePalsyImitation3D-v0', 40)]
+    cfg = {'integrator': 'rk-merson'}
+    mixed = MixedVectorEnv(segments, config=cfg, precision=64, seed=5, auto_reset=True)
+    alone, off = [], 0
+    for env_id, n in segments:
+        alone.append(VectorEnv(env_id, n, config=cfg, precision=64, seed=5, auto_reset=True, env_offset=off))
+        off += n
+    for e in mixed.envs + alone:
+        e.set_rk_budget(3)
+    mixed.reset()
+    for e in alone:
+        e.reset()
+    g = torch.Generator(device='cuda').manual_seed(7)
+    suspended = 0
+    for t in range(40):
+        a = torch.rand((mixed.num_envs, mixed.action_dim), generator=g, device=mixed.device, dtype=mixed.dtype)
+        obs, rew, done, _ = mixed.step(a)
+        for seg, e, o in zip(mixed.envs, alone, mixed.offsets):
+            sl = slice(o, o + e.num_envs)
+            eo, er, ed, _ = e.step(a[sl, :e.action_dim].contiguous())
+            assert torch.equal(seg.ready, e.ready), t
+            ok = e.ready.bool()
+            assert torch.equal(obs[sl, :e.obs_dim][ok], eo[ok]) and torch.equal(rew[sl][ok], er[ok]), t
+            assert torch.equal(done[sl][ok], ed[ok]), t
+            suspended += int((~ok).sum())
+    assert suspended > 0          # the budget suspended some steps: the resume path ran
+    assert sum(e.reset_count() for e in mixed.envs) == sum(e.reset_count() for e in alone)
+    for e in alone + [mixed]:
+        e.close()
