@@ -91,6 +91,51 @@ def test_realize_report_matches_oracle(env_id):
     env.close()
 
 
+@pytest.mark.parametrize('env_id,integrator,push', [('MuscleRunningImitation3D-v0', 'rk-merson', False),
+                                                   ('MuscleRunningImitation3D-v0', 'semi-implicit', True),
+                                                   ('MuscleRunningImitation3D-v0', 'rk-merson', True),
+                                                   ('MuscleLockedKneeImitation3D-v0', 'rk-merson', True),
+                                                   ('MuscleWalkingImitation2D-v0', 'rk-merson', True)])
+def test_realize_report_push_and_rk_kernels_match_oracle(env_id, integrator, push):
+    """The other force-report (REP) kernel variants — with the reference
+    integrator, with the torso push, and both (round 4 took them off scratch:
+    compile-time mode, no pass-through state, rolled report loops, DESIGN.md
+    5.5): after 5 oracle steps under the same push table, the oracle's state
+    is loaded into the GPU env and the realize report of every env equals the
+    oracle's within 1e-9, as in test_realize_report_matches_oracle."""
+    import torch
+    from bioimitation.obslayout import load_names
+    from bioimitation.perturb import os_body_index, zoh_table
+    n = 16
+    rng = np.random.default_rng(11)
+    pk, env, orc, bufs = _pair(env_id, n, integrator)
+    rows = rng.integers(0, min(120, int(pk.reset_hi)) + 1, size=n)
+    if push:
+        x = np.arange(0.0, 3.0, 0.03) + 0.0013
+        y = rng.choice([-50.0, 0.0, 50.0], size=(n, len(x)))
+        env.set_perturbation(x, y)
+        ob = os_body_index(load_names(env_id))
+        xt, _ = zoh_table(x, y)
+        for i in range(n):
+            orc.set_perturbation(bufs, i, ob, xt, y[i])
+    env.reset(ref_index=rows)
+    for i in range(n):
+        orc.reset(bufs, i, int(rows[i]))
+    for t in range(5):
+        a = _acts(pk, rng, n, rows + t + 1) * (0.4 if pk.nmuscle else 1.0)
+        for i in range(n):
+            orc.step(bufs, i, a[i])
+    env.set_state(np.stack([orc.get_state(bufs, i) for i in range(n)]))
+    rep = env.osim('realize', np.arange(n)).cpu().numpy()
+    worst = 0.0
+    for i in range(n):
+        e = _rel(rep[i], orc.osim_report(bufs, i))
+        assert e.max() < 1e-9, (i, int(np.argmax(e)), e.max())
+        worst = max(worst, e.max())
+    print(f'{env_id} {integrator} push={push}: realize report max rel err {worst:.2e} over {n} envs')
+    env.close()
+
+
 @pytest.mark.parametrize('env_id', ['MuscleWalkingImitation2D-v0', 'TorqueWalkingImitation2D-v0',
                                     'MuscleRunningImitation3D-v0', 'MuscleLockedKneeImitation3D-v0'])
 def test_reference_reset_body_through_facade_matches_bioim_reset(env_id):
