@@ -261,19 +261,48 @@ def make(env_id, config=None, **kw):
     return ENV_CLASSES[env_id](config, **kw)
 
 
+# rllib_creator: the env offset of worker w's vector slot v is
+# (w << RLLIB_WORKER_SHIFT) + v * num_envs, distinct for up to 2**20 envs per worker
+RLLIB_WORKER_SHIFT = 20
+
+
+def _ray_vector_env_class():
+    """RLlibVectorEnv with ``ray.rllib.env.vector_env.VectorEnv`` as a base
+    class when ray is importable (RLlib's env conversion dispatches on
+    isinstance, so the duck-typed protocol alone would be taken for a
+    gym.Env), else None."""
+    try:
+        from ray.rllib.env.vector_env import VectorEnv as RayVectorEnv
+    except Exception:
+        return None
+    from .adapters import RLlibVectorEnv
+
+    class RayRLlibVectorEnv(RLlibVectorEnv, RayVectorEnv):
+        def __init__(self, *args, **kw):
+            RLlibVectorEnv.__init__(self, *args, **kw)
+            RayVectorEnv.__init__(self, self.observation_space, self.action_space, self.num_envs)
+    return RayRLlibVectorEnv
+
+
 def rllib_creator(env_id):
     """The env creator registered with Ray for ``env_id``
     (bioimitation/__init__.py:135-143 registers ``lambda config: Env(config)``).
     With ``config['num_envs'] > 1`` it returns one batched
     :class:`~bioimitation.adapters.RLlibVectorEnv` of that many envs on the
-    worker's GPU (RLlib uses an env that implements its VectorEnv protocol as
-    is), instead of one single-env instance per call: the reference's
+    worker's GPU, instead of one single-env instance per call: the reference's
     one-env-per-worker layout costs a kernel launch and a host round trip per
     env step (180 us per step against 45-56 us for one CPU thread
     running the same algorithm), the batched env amortizes both over the batch.
+    When ray is importable the returned object is also an instance of RLlib's
+    ``VectorEnv`` (:func:`_ray_vector_env_class`), which is what RLlib's env
+    conversion checks for.
     Optional keys: ``device`` (GPU ordinal, default 0), ``precision`` (64).
-    RLlib's EnvContext ``worker_index`` offsets the envs' global indices
-    (``env_offset``), so every worker draws its own reset rows."""
+    RLlib's EnvContext ``worker_index`` and ``vector_index`` (several creator
+    calls per worker when ``num_envs_per_worker > 1``) set the envs' global
+    indices (``env_offset`` = (worker_index << 20) + vector_index * num_envs),
+    so every worker and vector slot draws its own reset rows.
+    Ray is not importable here: the CPU tests cover the creator's dispatch
+    and offsets (tests/test_envs.py), not RLlib's own conversion."""
     if env_id not in ENV_CLASSES:
         if env_id in NOT_BUILT:
             raise NotImplementedError(f'{env_id}: {NOT_BUILT[env_id]}')
@@ -287,9 +316,20 @@ def rllib_creator(env_id):
             return cls(config)
         from .adapters import RLlibVectorEnv
         device, precision = int(cfg.pop('device', 0)), int(cfg.pop('precision', 64))
-        offset = int(getattr(config, 'worker_index', 0) or 0) * n
-        return RLlibVectorEnv(env_id, n, config=cfg, device=device, precision=precision, env_offset=offset)
+        offset = rllib_env_offset(config, n)
+        vcls = _ray_vector_env_class() or RLlibVectorEnv
+        return vcls(env_id, n, config=cfg, device=device, precision=precision, env_offset=offset)
     return create
+
+
+def rllib_env_offset(config, num_envs):
+    """Global index of the first env of the batch an RLlib creator call makes
+    (its EnvContext's worker_index and vector_index; 0 for a plain dict)."""
+    w = int(getattr(config, 'worker_index', 0) or 0)
+    v = int(getattr(config, 'vector_index', 0) or 0)
+    if v * num_envs >= (1 << RLLIB_WORKER_SHIFT):
+        raise ValueError(f'rllib_creator: vector_index {v} x num_envs {num_envs} exceeds 2**{RLLIB_WORKER_SHIFT} envs per worker')
+    return (w << RLLIB_WORKER_SHIFT) + v * num_envs
 
 
 def register_with_gym():

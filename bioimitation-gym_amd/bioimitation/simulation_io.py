@@ -421,31 +421,47 @@ class OsimModelFacade:
     def storage(self):
         """the last env step's accepted integration steps (RK; None otherwise).
         A step with more accepted steps than the buffer holds keeps its first
-        ``cap`` rows and warns: the recording is optional, the step itself is
-        complete (the reference just integrates)."""
+        ``cap`` rows: the rows past them were not recorded on the device, so
+        the step warns, counts them in ``storage_truncated_rows`` (reported
+        again by save_simulation) and grows the buffer to at least twice its
+        size for the later steps.  The step itself is complete (the reference
+        just integrates)."""
         env = self._env
         if getattr(env, 'storage_rows', None) is None:
             return None
         k = int(env.storage_count[self._i])
         cap = env.storage_rows.shape[1]
+        rows = env.storage_rows[self._i, :min(k, cap)].double().cpu().numpy()
         if k > cap:
-            warnings.warn(f'state storage: {k} accepted integration steps in one env step, the buffer holds '
-                          f'{cap}; the rows after the first {cap} are not recorded', RuntimeWarning)
-            k = cap
-        return env.storage_rows[self._i, :k].double().cpu().numpy()
+            self.storage_truncated_rows = getattr(self, 'storage_truncated_rows', 0) + (k - cap)
+            warnings.warn(f'state storage: {k} accepted integration steps in one env step, the buffer held '
+                          f'{cap}; the rows after the first {cap} are not recorded (buffer grown to '
+                          f'{max(2 * cap, k)} rows for the next steps)', RuntimeWarning)
+            env.enable_state_storage(max(2 * cap, k))
+        return rows
 
     def _realizer(self, k):
         """a batch of the same model (one env per stored state) on which the
-        accepted integration steps are realized; grown on demand"""
+        accepted integration steps are realized; grown on demand.  It carries
+        this env's torso push (the PrescribedForce the reference model holds):
+        the env's own row of its perturbation table on every scratch row, set
+        at each use (the env's table may have been replaced since), and never
+        a schedule of its own (``apply_perturbations`` off in its config)."""
+        e = self._env
         rz = getattr(self, '_rz', None)
         if rz is None or rz.num_envs < k:
             from .vector_env import VectorEnv
-            e = self._env
             if rz is not None:
                 rz.close()
-            rz = VectorEnv(e.env_id, max(k, 64), config=e.config, device=e.device.index, precision=e.precision)
+            cfg = dict(e.config or {}, apply_perturbations=False)
+            rz = VectorEnv(e.env_id, max(k, 64), config=cfg, device=e.device.index, precision=e.precision)
             rz.enable_force_report()
             self._rz = rz
+        if e.perturbation is not None:
+            x, y = e.perturbation
+            rz.set_perturbation(x, np.asarray(y)[self._i])
+        elif rz.perturbation is not None:
+            rz.set_perturbation(None, None)
         return rz
 
     def analysis_rows(self, storage):
@@ -570,5 +586,11 @@ class OsimModelFacade:
 
     def save_simulation(self, base_dir):
         """Writes simulation_States.sto, simulation_Kinematics_{q,u,dudt}.sto and
-        simulation_ForceReporter_forces.sto."""
+        simulation_ForceReporter_forces.sto.  If a state-storage overflow
+        dropped accepted integration steps (``storage``), the files miss those
+        rows against the reference's: warned again here, with the count."""
+        lost = getattr(self, 'storage_truncated_rows', 0)
+        if lost:
+            warnings.warn(f'save_simulation: {lost} accepted integration steps were not recorded '
+                          f'(state-storage overflow); the .sto files miss those rows', RuntimeWarning)
         return self.recorder.write(base_dir)

@@ -362,6 +362,12 @@ class MixedVectorEnv:
     def build_id(self) -> str:
         return self._L.bioim_build_id().decode()
 
+    @property
+    def last_step_fused(self) -> bool:
+        """whether the last ``step`` ran as ONE fused two-topology launch
+        (bioim_group_fused) rather than one launch per segment"""
+        return _lib.check(self._L.bioim_group_fused(self.envs[0]._h)) == 1
+
     def reset(self):
         for e in self.envs:
             e.reset()

@@ -92,6 +92,16 @@ DEV void sfor(F &&f) {
 #ifndef BIOIM_BF3_RK
 #define BIOIM_BF3_RK 1
 #endif
+/* fiber-velocity warm start (round-5 experiments): BIOIM_FV_HERMITE = cubic
+ * Hermite u(v) start from the table slopes instead of linear interpolation;
+ * BIOIM_FV_PRED = linear extrapolation of the previous two substeps' roots
+ * in the semi-implicit substep loop */
+#ifndef BIOIM_FV_HERMITE
+#define BIOIM_FV_HERMITE 0
+#endif
+#ifndef BIOIM_FV_PRED
+#define BIOIM_FV_PRED 0
+#endif
 template <typename Real> struct Eps;
 template <> struct Eps<float> {
     static constexpr float u_tol = 2e-7f;   /* Bezier parameter tolerance  */
@@ -526,7 +536,14 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
         i0 = i0 < 0 ? 0 : (i0 > BIOIM_UTAB - 1 ? BIOIM_UTAB - 1 : i0);
         Real fr = tt - Real(i0);
         const Real ua = C.ut[k][i0], ub = C.ut[k][i0 + 1];
+#if BIOIM_FV_HERMITE
+        /* the cubic Hermite start of curve_eval (table slopes mt) */
+        const Real ma = C.mt[k][i0], mb = C.mt[k][i0 + 1], dua = ub - ua;
+        const Real h2 = Real(3) * dua - Real(2) * ma - mb, h3 = ma + mb - Real(2) * dua;
+        const Real ut = fma(fr, fma(fr, fma(fr, h3, h2), ma), ua), us = ga * newton_rcp(ga - gb);
+#else
         const Real ut = ua + fr * (ub - ua), us = ga * newton_rcp(ga - gb);
+#endif
         u = ((v0 > xa) & (v0 < xb)) ? ut : us;
     }
     const Real half = 0.5;
@@ -2537,6 +2554,11 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
     Dyn<T, Real> D;
 #pragma unroll
     for (int j = 0; j < MPL; ++j) D.ms[j].vN = 0;
+#if BIOIM_FV_PRED
+    Real vprev[MPL];
+#pragma unroll
+    for (int j = 0; j < MPL; ++j) vprev[j] = 0;
+#endif
     /* lane d < ND owns dof d (coordinate value qd, speed ud) */
     Real qd = 0, ud = 0;
     if (lane < ND) { qd = GAT(st.q, (size_t)lane * N + env, (size_t)ND * N); ud = GAT(st.u, (size_t)lane * N + env, (size_t)ND * N); }
@@ -2802,6 +2824,16 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                 const double cs = rk_stage == 0 ? 0.0 : rk_stage <= 2 ? 1.0 / 3.0 : rk_stage == 3 ? 0.5 : 1.0;
                 pslot[0] = rk_t + cs * rk_h; pslot[1] = 0;
             }
+#if BIOIM_FV_PRED
+            if constexpr (!RK && NM > 0) {
+#pragma unroll
+                for (int j = 0; j < MPL; ++j) {
+                    const Real vc = D.ms[j].vN;
+                    D.ms[j].vN = vc + (vc - vprev[j]);
+                    vprev[j] = vc;
+                }
+            }
+#endif
             /* RK: explicit accelerations (h = 0, the implicit terms compile away) */
             /* branch-free phase-3 row stores, except in the spatial RK kernels
              * (they would take those kernels past the 512-register budget) */
@@ -3641,6 +3673,7 @@ struct bioim_handle {
     int rk_budget;      /* RK attempts per env per launch, 0: unbudgeted (bioim_set_rk_budget) */
     uint8_t *ready_out; /* caller's device buffer [n] or null */
     const uint8_t *active; /* caller's device buffer [n] or null (bioim_set_active_mask) */
+    int last_group_fused; /* the last bioim_step_group with this handle first ran one fused launch */
     Ops ops;
     bioim_modelpack_t pack;
 };
@@ -4146,6 +4179,11 @@ int bioim_set_group_fusion(int on) {
     return 0;
 }
 
+int bioim_group_fused(const bioim_handle_t *h) {
+    if (!h) return fail(BIOIM_E_ARG, "bioim_group_fused: null handle");
+    return h->last_group_fused ? 1 : 0;
+}
+
 int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs, void *reward, uint8_t *done,
                      void *info) {
     if (!hs || nh <= 0 || !actions || !done) return fail(BIOIM_E_ARG, "bioim_step_group: bad arguments");
@@ -4162,11 +4200,13 @@ int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs
     /* two segments whose topology pair has a fused kernel (BIOIM_FUSED_PAIRS)
      * and that run the default step kernels (no push table, semi-implicit):
      * one launch, workgroups [0, B0) segment 0, the rest segment 1 */
+    hs[0]->last_group_fused = 0;
     if (nh == 2 && g_group_fusion && hs[0]->pert_n == 0 && hs[1]->pert_n == 0 && !hs[0]->rk && !hs[1]->rk) {
         const int rc = bioim_fused_launch(hs[0], hs[1], actions, obs, reward, done, info);
         if (rc < 0) return rc;
         if (rc == 1) {
             HIPCHK(hipGetLastError());
+            hs[0]->last_group_fused = 1;
             return 0;
         }
     }

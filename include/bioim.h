@@ -106,6 +106,12 @@ int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs
  * (default on; off: one concurrent launch per segment).  Results are the
  * same bit for bit either way. */
 int bioim_set_group_fusion(int on);
+/* 1 if the last bioim_step_group call with h as its first handle ran as ONE
+ * fused two-topology launch, 0 if it ran one launch per segment (or no group
+ * step yet); -1 for a null handle.  Lets callers and tests see that the
+ * fused kernel really ran (it falls back to per-segment launches for fp32,
+ * a push table, RK-Merson or a pair without a fused kernel). */
+int bioim_group_fused(const bioim_handle_t *h);
 /* apply_perturbations (muscle_walking_imitation_env2D.py:83-100 and the same
  * block in every task env): a PrescribedForce on the torso whose ground-frame
  * x force is a PiecewiseConstantFunction of simulation time.  Here: a

@@ -180,8 +180,10 @@ def test_rllib_creator_dispatches_on_num_envs(monkeypatch):
     ``lambda config: Env(config)``) returns the single-env class for the
     reference's configs and one batched RLlibVectorEnv when the env config
     asks for num_envs > 1 (device / precision passed through, the worker
-    index offsetting the global env indices).  Host logic only: both
-    constructors are replaced by recorders."""
+    and vector indices offsetting the global env indices).  Host logic
+    only: both constructors are replaced by recorders; ray is not importable
+    here, so the RLlib VectorEnv base class (envs._ray_vector_env_class) is
+    checked with a stand-in module."""
     from bioimitation import adapters, envs
     calls = []
 
@@ -193,8 +195,12 @@ def test_rllib_creator_dispatches_on_num_envs(monkeypatch):
         def __init__(self, env_id, num_envs, config=None, device=0, precision=64, seed=0, env_offset=0):
             calls.append(('vec', env_id, num_envs, dict(config or {}), device, precision, env_offset))
 
-    class EnvContext(dict):          # ray.rllib.env.EnvContext: a dict with worker_index
+    class EnvContext(dict):          # ray.rllib.env.EnvContext: a dict with worker_index / vector_index
         worker_index = 3
+        vector_index = 0
+
+    class EnvContextV(EnvContext):   # the second sub-env of worker 3 (num_envs_per_worker > 1)
+        vector_index = 1
 
     env_id = 'MuscleWalkingImitation2D-v0'
     monkeypatch.setitem(envs.ENV_CLASSES, env_id, Single)
@@ -203,8 +209,47 @@ def test_rllib_creator_dispatches_on_num_envs(monkeypatch):
     create({'mode': 'test'})
     create(EnvContext(num_envs=1, horizon=3))
     create(EnvContext(num_envs=256, device=1, precision=32, horizon=3))
+    create(EnvContextV(num_envs=256, horizon=3))
     assert calls[0] == ('single', {'mode': 'test'})
     assert calls[1] == ('single', {'num_envs': 1, 'horizon': 3})
-    assert calls[2] == ('vec', env_id, 256, {'horizon': 3}, 1, 32, 3 * 256)
+    assert calls[2] == ('vec', env_id, 256, {'horizon': 3}, 1, 32, 3 << envs.RLLIB_WORKER_SHIFT)
+    # a worker's vector slots get disjoint env ranges
+    assert calls[3] == ('vec', env_id, 256, {'horizon': 3}, 0, 64, (3 << envs.RLLIB_WORKER_SHIFT) + 256)
+    with pytest.raises(ValueError):
+        envs.rllib_env_offset(EnvContextV(), 1 << envs.RLLIB_WORKER_SHIFT)
     with pytest.raises(NotImplementedError):
         envs.rllib_creator('MuscleJumpingImitation2D-v0')
+
+
+def test_rllib_vector_env_class_derives_from_ray(monkeypatch):
+    """with ray importable the batched creator's class is also an
+    instance of ray.rllib.env.vector_env.VectorEnv (RLlib's env conversion
+    dispatches on isinstance).  A stand-in ray module records the base
+    class's constructor arguments; no GPU (RLlibVectorEnv's own constructor
+    is replaced)."""
+    import sys
+    import types
+    from bioimitation import adapters, envs
+    seen = []
+
+    class RayVectorEnv:
+        def __init__(self, observation_space, action_space, num_envs):
+            seen.append((observation_space, action_space, num_envs))
+
+    mods = {}
+    for name in ('ray', 'ray.rllib', 'ray.rllib.env', 'ray.rllib.env.vector_env'):
+        mods[name] = types.ModuleType(name)
+    mods['ray.rllib.env.vector_env'].VectorEnv = RayVectorEnv
+    for k, v in mods.items():
+        monkeypatch.setitem(sys.modules, k, v)
+
+    def fake_init(self, env_id, num_envs, config=None, device=0, precision=64, seed=0, env_offset=0):
+        self.num_envs, self.observation_space, self.action_space = num_envs, 'obs', 'act'
+    monkeypatch.setattr(adapters.RLlibVectorEnv, '__init__', fake_init)
+    cls = envs._ray_vector_env_class()
+    assert cls is not None and issubclass(cls, RayVectorEnv) and issubclass(cls, adapters.RLlibVectorEnv)
+    v = cls('MuscleWalkingImitation2D-v0', 8)
+    assert isinstance(v, RayVectorEnv) and seen == [('obs', 'act', 8)]
+    monkeypatch.delitem(sys.modules, 'ray.rllib.env.vector_env')
+    monkeypatch.setitem(sys.modules, 'ray', None)
+    assert envs._ray_vector_env_class() is None

@@ -351,7 +351,8 @@ def test_rk_state_storage_rows_match_oracle(tmp_path):
     env.close()
 
 
-def test_rk_analyses_record_every_integration_step(tmp_path):
+@pytest.mark.parametrize('push', [False, True])
+def test_rk_analyses_record_every_integration_step(tmp_path, push):
     """With the reference's integrator OpenSim's Kinematics and ForceReporter
     analyses record at every accepted integration step, like the Manager's
     state storage (opensim_wrapper.py:10-15, :334-338).  Each of the GPU's
@@ -361,9 +362,13 @@ def test_rk_analyses_record_every_integration_step(tmp_path):
     the oracle's realize of the oracle's stored states (1e-6 relative to
     max(|x|, 1): the step sizes agree to the rounding level, q'' near contact
     carries its conditioning), and the four .sto files hold one row per
-    accepted step plus the initial state."""
+    accepted step plus the initial state.  ``push``: the env carries a torso
+    push (apply_perturbations' PrescribedForce, muscle_walking_imitation_env2D.py:83-100)
+    and the scratch batch must realize the stored states with it too."""
     import oracle
     from bioimitation import envs
+    from bioimitation.obslayout import load_names
+    from bioimitation.perturb import os_body_index, zoh_table
     from bioimitation.simulation_io import split_osim_report
     from bioimitation.storage import read_sto
     env_id = 'MuscleWalkingImitation2D-v0'
@@ -372,13 +377,19 @@ def test_rk_analyses_record_every_integration_step(tmp_path):
     pk = env._env.pack
     nd, nm = pk.ndof, pk.nmuscle
     orc = oracle.Oracle(pk)
-    bufs, scratch = orc.new_envs(1), orc.new_envs(1)
+    bufs, scratch, bare = orc.new_envs(1), orc.new_envs(1), orc.new_envs(1)
+    if push:   # a push held at every time, so every stored state carries it
+        x, y = np.linspace(0.0, 10.0, 100), np.full(100, -50.0)
+        env._env.set_perturbation(x, y[None, :])
+        ob = os_body_index(load_names(env_id))
+        orc.set_perturbation(bufs, 0, ob, *zoh_table(x, y))
+        orc.set_perturbation(scratch, 0, ob, *zoh_table(x, y))
     orc.set_integrator(bufs, 0, 'rk-merson', 1e-3)
     orc.reset(bufs, 0, 0)
     store = np.zeros((512, 1 + 2 * nd + 2 * nm))
     orc.set_state_storage(bufs, 0, store)
     rng = np.random.default_rng(4)
-    want_qdd, want_f = [], []
+    want_qdd, want_f, bare_qdd = [], [], []
     for t in range(5):
         a = rng.uniform(0.0, 0.6, size=pk.nact)
         env.step(a)
@@ -391,6 +402,10 @@ def test_rk_analyses_record_every_integration_step(tmp_path):
             orc.set_state(scratch, 0, s)
             want_qdd.append(split_osim_report(pk, orc.osim_report(scratch, 0))['qdd'])
             want_f.append(orc.force_report(scratch, 0))
+            orc.set_state(bare, 0, s)
+            bare_qdd.append(split_osim_report(pk, orc.osim_report(bare, 0))['qdd'])
+    # the push is visible in q'' (the test can tell a scratch batch without it)
+    assert (np.abs(np.array(bare_qdd) - np.array(want_qdd)).max() > 1e-3) == push
     rec = env.osim_model.recorder
     nc = pk.ncoord
     got_qdd = np.array([r[1 + 2 * nc:1 + 3 * nc] for r in rec.rows[1:]])
@@ -422,4 +437,39 @@ def test_empty_and_duplicate_env_lists():
         with pytest.raises(ValueError):
             env.reset(env_ids=bad)
     np.testing.assert_array_equal(env.get_state(), before)
+    env.close()
+
+
+def test_state_storage_overflow_grows_buffer(tmp_path):
+    """an env step with more accepted RK steps than the state
+    storage holds keeps its first ``cap`` rows, warns, counts the lost rows
+    (save_simulation warns with them) and grows the buffer, so the next
+    step records every row again."""
+    import warnings
+    from bioimitation import envs
+    env = envs.make('MuscleWalkingImitation2D-v0', config={'integrator': 'rk-merson', 'mode': 'test'})
+    env.reset()
+    env._env.enable_state_storage(2)
+    a = np.full(14, 0.3)
+    with pytest.warns(RuntimeWarning, match='state storage'):
+        env.step(a)
+    om = env.osim_model
+    lost = om.storage_truncated_rows
+    assert lost > 0 and env._env.storage_rows.shape[1] >= 4
+    assert env._env.storage_rows.shape[1] >= int(env._env.storage_count[0])
+    clean = False
+    for _ in range(6):   # a later step may overflow the grown buffer too: it grows again
+        n0 = len(om.recorder.rows)
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter('always')
+            env.step(a)
+        if not w:
+            k = int(env._env.storage_count[0])
+            assert 0 < k <= env._env.storage_rows.shape[1] and len(om.recorder.rows) - n0 == k
+            clean = True
+            break
+    assert clean
+    lost = om.storage_truncated_rows
+    with pytest.warns(RuntimeWarning, match=f'{lost} accepted integration steps'):
+        om.save_simulation(str(tmp_path))
     env.close()

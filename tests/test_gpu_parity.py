@@ -256,12 +256,12 @@ def test_mixed_batch_matches_separate_envs(segments, fusion):
     from bioimitation import _lib
     _lib.load().bioim_set_group_fusion(fusion)
     try:
-        _mixed_batch_check(segments)
+        _mixed_batch_check(segments, fused=bool(fusion) and len(segments) == 2)
     finally:
         _lib.load().bioim_set_group_fusion(1)      # the process-wide default
 
 
-def _mixed_batch_check(segments):
+def _mixed_batch_check(segments, fused=False):
     import torch
     from bioimitation.vector_env import MixedVectorEnv, VectorEnv
     mixed = MixedVectorEnv(segments, precision=64, seed=21, auto_reset=True)
@@ -280,6 +280,7 @@ def _mixed_batch_check(segments):
         a = torch.rand((mixed.num_envs, mixed.action_dim), generator=g, device=mixed.device, dtype=mixed.dtype)
         acts.append(a)
         obs, rew, done, info = mixed.step(a)
+        assert mixed.last_step_fused == fused, (t, fused)   # the fused kernel really ran
         trace.append(obs.clone())
         for e, o in zip(alone, mixed.offsets):
             sl = slice(o, o + e.num_envs)
@@ -296,6 +297,61 @@ def _mixed_batch_check(segments):
     assert mixed.action_mask.sum().item() == sum(e.num_envs * e.action_dim for e in alone)
     for e in alone + [mixed]:
         e.close()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+def test_c5_fused_launch_at_bench_size_vs_oracle():
+    """config C5 at the size the bench runs — 2048
+    LockedKnee3D + 2048 Palsy3D envs in ONE fused launch (env_kernel2, 256
+    workgroups split by segment; the launch is asserted fused) — against the
+    oracle on a strided sample that holds the first and last workgroup of
+    each segment and the workgroups on either side of the segment boundary,
+    6 steps, auto-reset off, obs / reward / info within 1e-6."""
+    import torch
+    import oracle
+    from bioimitation import _lib
+    from bioimitation.registry import load_pack
+    from bioimitation.vector_env import MixedVectorEnv
+    segs = [('MuscleLockedKneeImitation3D-v0', 2048), ('MusclePalsyImitation3D-v0', 2048)]
+    _lib.load().bioim_set_group_fusion(1)
+    mixed = MixedVectorEnv(segs, precision=64, seed=9, auto_reset=False)
+    epw = mixed.envs[0].launch['envs_per_workgroup']
+    rng = np.random.default_rng(46)
+    checks = []
+    for (env_id, n), e, off in zip(segs, mixed.envs, mixed.offsets):
+        pk = load_pack(env_id)
+        rows = rng.integers(0, pk.reset_hi + 1, size=n)
+        e.reset(ref_index=rows)
+        # local indices: first and last workgroup, every 97th env
+        loc = np.unique(np.concatenate([np.arange(epw), np.arange(n - epw, n), np.arange(0, n, 97)]))
+        orc = oracle.Oracle(pk)
+        bufs = orc.new_envs(len(loc))
+        for j, i in enumerate(loc):
+            orc.reset(bufs, j, int(rows[i]))
+        checks.append((env_id, e, off, loc, orc, bufs, np.ones(len(loc), bool)))
+    # the boundary: global envs 2032..2063 = the last workgroup of segment 0 and the first of segment 1
+    assert mixed.offsets[1] == 2048 and mixed.offsets[1] % epw == 0
+    worst, nchk = 0.0, 0
+    for t in range(6):
+        acts = rng.uniform(0.0, 1.0, size=(mixed.num_envs, mixed.action_dim))
+        obs, rew, done, info = mixed.step(torch.as_tensor(acts, device=mixed.device))
+        assert mixed.last_step_fused, 'the C5 pair must run as one fused launch'
+        obs, rew, done, info = (x.cpu().numpy() for x in (obs, rew, done, info))
+        assert np.isfinite(obs).all()
+        for env_id, e, off, loc, orc, bufs, alive in checks:
+            for j, i in enumerate(loc):
+                if not alive[j]:
+                    continue
+                g = off + i
+                o, r, d, inf = orc.step(bufs, j, acts[g, :e.action_dim])
+                err = max(_rel(obs[g, :e.obs_dim], o).max(), abs(rew[g] - r), _rel(info[g, :e.info_dim], inf).max())
+                assert err < 1e-6, (env_id, t, int(i), err)
+                assert bool(done[g]) == d, (env_id, t, int(i))
+                worst = max(worst, err)
+                nchk += 1
+                alive[j] = not d
+    print(f'C5 fused 2048 + 2048 envs x 6 steps: {nchk} env-steps checked, max rel err {worst:.2e}')
+    mixed.close()
 
 
 @pytest.mark.skipif(not gpu_available(), reason='needs GPU')
@@ -681,6 +737,69 @@ def test_parity_200_steps_c3_tracking_drive():
     assert e_gpu.max() < 1e-4, (int(e_gpu.argmax()), e_gpu.max())
     assert (e_gpu <= np.maximum(1e-7, 100 * e_twin)).all(), int(np.argmax(e_gpu / np.maximum(1e-30, e_twin)))
     assert orc_alive.sum() >= n // 2 and gpu_alive.sum() >= n // 2, (orc_alive.sum(), gpu_alive.sum())
+    env.close()
+
+
+# fp32 free-running on the C3 tracking drive: the stated
+# fp64 -> fp32 tolerance of north_star, measured on the one drive whose fp64
+# trajectories are not chaotic (oracle twin ~1e-10 over 200 steps).  Bounds
+# per column class, relative to max(|x|, 1), over env-steps alive on both
+# sides (DESIGN.md section 2 quotes the measured values).
+FP32_FREE_TOL = {'state': None, 'rate': None, 'qdd': None, 'reward': None}
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+def test_fp32_free_running_c3_tracking_drive():
+    """The HIP path at precision 32, free-running (never re-synced), on the
+    C3 tracking drive (tests/tracking.py) against the fp64 oracle for 200
+    steps: the same 32 reset rows and drive as the fp64 test above, actions
+    computed from the oracle's state and sent (rounded to fp32) to both
+    sides.  Reports the error per column class and step; asserts the bounds
+    in FP32_FREE_TOL (None: report only)."""
+    import torch
+    from tracking import ROWS_FALL, ROWS_UP, TrackingDrive
+    from bioimitation.obslayout import column_names, load_names
+    env_id = 'MuscleWalkingImitation2D-v0'
+    rows = np.array(ROWS_UP + ROWS_FALL)
+    n, T = len(rows), 200
+    pk, env, orc, bufs = _setup(env_id, n, 32)
+    drive = TrackingDrive(orc, pk, load_names(env_id))
+    env.reset(ref_index=rows)
+    for i in range(n):
+        orc.reset(bufs, i, int(rows[i]))
+    names = column_names(pk, load_names(env_id))
+    qdd = _qdd_cols(pk)
+    other = np.setdiff1d(np.arange(env.obs_dim), qdd)
+    rate = np.array([names[c].startswith(('coordinate_vel', 'body_vel', 'contact_forces')) or
+                     names[c].endswith('fiber_velocity') for c in other])
+    live = np.ones(n, bool)
+    err = {k: np.zeros(T) for k in ('state', 'rate', 'qdd', 'reward')}
+    col = np.zeros(len(other))
+    done_mismatch = 0
+    for t in range(T):
+        acts = np.stack([drive(orc.get_state(bufs, i)) for i in range(n)]).astype(np.float32).astype(np.float64)
+        obs, rew, done = (v.cpu().numpy().astype(np.float64) for v in
+                          env.step(torch.as_tensor(acts, device=env.device, dtype=torch.float32))[:3])
+        for i in range(n):
+            o, r, d, _ = orc.step(bufs, i, acts[i])
+            if live[i]:
+                e = _rel(obs[i], o)
+                col = np.maximum(col, e[other])
+                err['state'][t] = max(err['state'][t], e[other][~rate].max())
+                err['rate'][t] = max(err['rate'][t], e[other][rate].max())
+                err['qdd'][t] = max(err['qdd'][t], e[qdd].max())
+                err['reward'][t] = max(err['reward'][t], abs(rew[i] - r) / max(1.0, abs(r)))
+                done_mismatch += int(bool(done[i]) != d)
+            live[i] = live[i] and not (d or bool(done[i]))
+    ks = [0, 49, 99, 149, 199]
+    print(f'{env_id} fp32 free-running vs fp64 oracle, tracking drive, {n} envs x {T} steps '
+          f'({live.sum()} live at t=200, {done_mismatch} done mismatches): ' +
+          '; '.join(f'{k} ' + ', '.join(f't={j + 1} {err[k][j]:.1e}' for j in ks) + f' max {err[k].max():.1e}'
+                    for k in err) + f'; worst columns {_worst_columns(env_id, pk, col, other)}')
+    for k, tol in FP32_FREE_TOL.items():
+        assert np.isfinite(err[k]).all()
+        if tol is not None:
+            assert err[k].max() < tol, (k, err[k].max(), tol)
     env.close()
 
 
