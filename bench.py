@@ -207,6 +207,8 @@ def main():
     ap.add_argument('--mixed', default=None,
                     help="mixed batch 'ID_A,ID_B' split 50/50 per GPU (BASELINE config C5), e.g. "
                          "MuscleLockedKneeImitation3D-v0,MusclePalsyImitation3D-v0")
+    ap.add_argument('--no-reset-table', action='store_true',
+                    help='run every in-kernel auto-reset as a reset realize in the step launch (bioim_set_reset_table 0)')
     ap.add_argument('--no-fuse', action='store_true',
                     help='mixed batch: concurrent per-segment launches instead of the fused two-topology kernel')
     ap.add_argument('--share-gpu', action='store_true',
@@ -261,6 +263,8 @@ def main():
         handles = [env]
         if a.rk_budget:
             env.set_rk_budget(a.rk_budget)
+    for h in handles:
+        h.set_reset_table(not a.no_reset_table)
     n, A = a.envs, env.action_dim
     pool = 64      # action batches cycled through (uploaded once; inputs resident in HBM)
     gen = np.random.Generator(np.random.PCG64(rank))
@@ -350,7 +354,8 @@ def main():
                        (f'nsub={env.nsub}' if a.integrator == 'semi-implicit' else 'RK-Merson 1e-3') + ', auto-reset',
                        'integrator': a.integrator, 'rk_budget': a.rk_budget or None,
                        'envs_per_gpu': n, 'lanes_per_env': env.lanes_per_env, 'parallelism': f'env-shard x{world}',
-                       'launch': env.launch, **({'group_fusion': not a.no_fuse} if a.mixed else {})},
+                       'launch': env.launch, 'reset_table': not a.no_reset_table,
+                       **({'group_fusion': not a.no_fuse} if a.mixed else {})},
             'roofline': roofline,
         }
         valu = _profile_record('valu.json', key, build_id)

@@ -118,6 +118,18 @@ class VectorEnv:
         _lib.check(self._L.bioim_set_perturbation(self._h, ob, len(xt), xt.ctypes.data_as(dp), yt.ctypes.data_as(dp)))
         self.perturbation = (np.asarray(x, dtype=np.float64), yt)
 
+    def set_reset_table(self, on: bool = True):
+        """In-kernel auto-resets from the per-handle reset table (default on;
+        bioim_set_reset_table): muscle models with the default step kernels
+        read the drawn row's reset state and observation instead of running
+        the reset realize in the step launch."""
+        _lib.check(self._L.bioim_set_reset_table(self._h, 1 if on else 0))
+
+    @property
+    def reset_table_rows(self) -> int:
+        """rows of the built reset table (0: not built / not used)"""
+        return _lib.check(self._L.bioim_reset_table_rows(self._h))
+
     def _bind_stream(self):
         """Launch on torch's current stream of the env's device (re-bound
         whenever the caller has switched streams since the last launch)."""

@@ -2290,6 +2290,14 @@ template <class T, typename Real> struct LaunchArgs {
     int osim_op, osim_dim;
     const Real *controls_in;
     Real *osim_out;
+    /* optional (default step kernels of muscle models, no push, no force
+     * report): the reset table — per reference row r its equilibrium fiber
+     * lengths [nmuscle] and reset observation [obs_dim] (row stride
+     * reset_tab_dim), computed once per handle by the reset realize itself
+     * (build_reset_table); an in-kernel auto-reset reads row r instead of
+     * running that realize again */
+    const Real *reset_tab;
+    int reset_tab_dim;
 };
 
 /* Reference integrator (RK kernels): OpenSim's Manager integrates with an
@@ -3166,6 +3174,35 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             pending_reset = true;
             do_reset = true;
             reset_row = draw_index(a.seed, a.env_offset + env, resets, M.reset_hi);
+            if constexpr (!RK && !PERT && !REP && NM > 0) {
+                /* the reset table (LaunchArgs::reset_tab): the state the reset
+                 * realize would leave (reference row, default activation,
+                 * equilibrium fiber lengths) and its observation, without a
+                 * dynamics call and fiber equilibrium in this wave — they made
+                 * the launch wait for its slowest wave */
+                if (a.reset_tab) {
+                    const int r = clamp_row(reset_row, M.nrows);
+                    const Real *tr = a.reset_tab + (size_t)r * a.reset_tab_dim;
+                    if (lane < ND) {
+                        const int c = SM.dof_coord[lane];
+                        qd = M.ref_q[r][c];
+                        ud = M.ref_u[r][c];
+                    }
+                    t = M.ref_time[r];
+                    istep = M.ref_istep[r];
+                    has_last = 0;
+                    resets += 1;
+#pragma unroll
+                    for (int j = 0; j < MPL; ++j) {
+                        const int m = mslot<T>(lane + j * G);
+                        if (m < NM) { act[j] = SM.mus[m].default_act; lce[j] = tr[m]; }
+                    }
+                    if (obs)
+                        for (int k = lane; k < M.obs_dim; k += G)
+                            GAT(obs, (size_t)env * a.obs_stride + k, (size_t)N * a.obs_stride) = tr[NM + k];
+                    break;
+                }
+            }
             continue;
         }
         break;
@@ -3674,9 +3711,19 @@ struct bioim_handle {
     uint8_t *ready_out; /* caller's device buffer [n] or null */
     const uint8_t *active; /* caller's device buffer [n] or null (bioim_set_active_mask) */
     int last_group_fused; /* the last bioim_step_group with this handle first ran one fused launch */
+    void *reset_tab;      /* Real [pack.nrows][nmuscle + obs_dim] or null (build_reset_table) */
+    int reset_tab_on;     /* bioim_set_reset_table (default 1) */
     Ops ops;
     bioim_modelpack_t pack;
 };
+
+/* the launches that read the reset table: steps of a muscle model with the
+ * default kernels (no push table, semi-implicit) and no force report or
+ * state storage (their rows come from the reset realize itself) */
+static inline bool reset_table_wanted(const bioim_handle_t *h) {
+    return h->reset_tab_on && h->auto_reset && h->nmuscle > 0 && h->pert_n == 0 && !h->rk && !h->force_out && !h->traj;
+}
+static inline bool reset_table_eligible(const bioim_handle_t *h) { return h->reset_tab && reset_table_wanted(h); }
 
 namespace {
 
@@ -3729,6 +3776,8 @@ LaunchArgs<T, Real> make_args(bioim_handle_t *h, int mode, const void *actions, 
     a.osim_dim = osim_report_dim(h->pack);
     a.controls_in = oc ? reinterpret_cast<const Real *>(oc->controls) : nullptr;
     a.osim_out = oc ? reinterpret_cast<Real *>(oc->report) : nullptr;
+    a.reset_tab = mode == 0 && reset_table_eligible(h) ? reinterpret_cast<const Real *>(h->reset_tab) : nullptr;
+    a.reset_tab_dim = h->nmuscle + h->obs_dim;
     return a;
 }
 
@@ -4024,6 +4073,7 @@ int bioim_create(const bioim_modelpack_t *pack, int n_envs, int device, int prec
     h->obs_dim = pack->obs_dim; h->info_dim = pack->info_dim; h->nsub = pack->nsub; h->auto_reset = 0;
     h->env_offset = 0;
     h->pert_n = 0; h->pert_ob = -1;
+    h->reset_tab = nullptr; h->reset_tab_on = 1;
     h->act_stride = pack->nact; h->obs_stride = pack->obs_dim; h->info_stride = pack->info_dim;
     h->ops = ops;
     memcpy(&h->pack, pack, sizeof(bioim_modelpack_t));
@@ -4052,6 +4102,7 @@ int bioim_destroy(bioim_handle_t *h) {
     if (h->smodel) hipFree(h->smodel);
     if (h->pert_x) hipFree(h->pert_x);
     if (h->pert_y) hipFree(h->pert_y);
+    if (h->reset_tab) hipFree(h->reset_tab);
     if (h->dstate) {
         if (h->precision == 64) delete reinterpret_cast<DState<double> *>(h->dstate);
         else delete reinterpret_cast<DState<float> *>(h->dstate);
@@ -4074,9 +4125,77 @@ int bioim_reset(bioim_handle_t *h, const int32_t *env_ids, const int32_t *ref_in
     return 0;
 }
 
+/* The reset table of a muscle-model handle (LaunchArgs::reset_tab), built
+ * once, on the first step that can use it: a scratch handle of the same pack
+ * and precision with one env per reference row is reset to row r (mode 1 —
+ * the very reset realize with fiber equilibrium an auto-reset runs), and its
+ * fiber lengths and observations are kept.  A reset realize depends on the
+ * row alone for these models: the held excitations enter only the activation
+ * rate, which the observation does not hold; the fiber-velocity root differs
+ * from a warm-started one at the rounding level only (its start is cold). */
+static int build_reset_table(bioim_handle_t *h) {
+    const int nr = h->pack.nrows, nm = h->nmuscle, od = h->obs_dim, nd = h->ndof;
+    const size_t R = h->precision == 64 ? 8 : 4, dim = (size_t)nm + od;
+    bioim_handle_t *tmp = nullptr;
+    int rc = bioim_create(&h->pack, nr, h->device, h->precision, h->seed, &tmp);
+    if (rc) return rc;
+    int32_t *d_idx = nullptr;
+    void *d_obs = nullptr, *d_tab = nullptr;
+    std::vector<int32_t> idx(nr);
+    for (int r = 0; r < nr; ++r) idx[r] = r;
+    const int sdim = bioim_state_dim(tmp);
+    std::vector<double> st((size_t)nr * sdim);
+    std::vector<unsigned char> obs((size_t)nr * od * R), tab((size_t)nr * dim * R);
+    auto done = [&](int code) {
+        if (d_idx) hipFree(d_idx);
+        if (d_obs) hipFree(d_obs);
+        if (code && d_tab) hipFree(d_tab);
+        bioim_destroy(tmp);
+        return code;
+    };
+    if (hipMalloc(&d_idx, sizeof(int32_t) * nr) != hipSuccess || hipMalloc(&d_obs, (size_t)nr * od * R) != hipSuccess ||
+        hipMalloc(&d_tab, (size_t)nr * dim * R) != hipSuccess ||
+        hipMemcpy(d_idx, idx.data(), sizeof(int32_t) * nr, hipMemcpyHostToDevice) != hipSuccess)
+        return done(fail(BIOIM_E_DEVICE, "build_reset_table: allocation failed"));
+    if ((rc = bioim_reset(tmp, nullptr, d_idx, nr, d_obs)) != 0) return done(rc);
+    if (hipStreamSynchronize(tmp->stream) != hipSuccess ||
+        hipMemcpy(obs.data(), d_obs, obs.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        return done(fail(BIOIM_E_DEVICE, "build_reset_table: reset realize failed"));
+    if ((rc = bioim_get_state(tmp, st.data())) != 0) return done(rc);
+    for (int r = 0; r < nr; ++r) {
+        unsigned char *row = tab.data() + (size_t)r * dim * R;
+        for (int m = 0; m < nm; ++m) {
+            const double l = st[(size_t)r * sdim + 5 + 2 * nd + nm + m];   /* fiber_length[m] */
+            if (R == 8) memcpy(row + m * R, &l, 8);
+            else { const float f = (float)l; memcpy(row + m * R, &f, 4); }
+        }
+        memcpy(row + (size_t)nm * R, obs.data() + (size_t)r * od * R, (size_t)od * R);
+    }
+    if (hipMemcpy(d_tab, tab.data(), tab.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return done(fail(BIOIM_E_DEVICE, "build_reset_table: upload failed"));
+    h->reset_tab = d_tab;
+    return done(0);
+}
+static int ensure_reset_table(bioim_handle_t *h) {
+    if (h->reset_tab || !reset_table_wanted(h)) return 0;
+    return build_reset_table(h);
+}
+
+int bioim_set_reset_table(bioim_handle_t *h, int on) {
+    if (!h) return fail(BIOIM_E_ARG, "bioim_set_reset_table: null handle");
+    h->reset_tab_on = on ? 1 : 0;
+    return 0;
+}
+
+int bioim_reset_table_rows(const bioim_handle_t *h) {
+    if (!h) return fail(BIOIM_E_ARG, "bioim_reset_table_rows: null handle");
+    return h->reset_tab ? h->pack.nrows : 0;
+}
+
 int bioim_step(bioim_handle_t *h, const void *actions, void *obs, void *reward, uint8_t *done, void *info) {
     if (!h || !actions || !done) return fail(BIOIM_E_ARG, "bioim_step: null handle/actions/done");
     HIPCHK(hipSetDevice(h->device));
+    if (const int rc = ensure_reset_table(h)) return rc;
     h->ops.launch(h, 0, actions, obs, reward, done, info, nullptr, nullptr, 0, nullptr);
     HIPCHK(hipGetLastError());
     return 0;
@@ -4195,6 +4314,8 @@ int bioim_step_group(bioim_handle_t **hs, int nh, const void *actions, void *obs
             return fail(BIOIM_E_ARG, "bioim_step_group: handles differ in device, precision or I/O strides");
     }
     HIPCHK(hipSetDevice(hs[0]->device));
+    for (int i = 0; i < nh; ++i)
+        if (const int rc = ensure_reset_table(hs[i])) return rc;
     const size_t R = hs[0]->precision == 64 ? 8 : 4;
     hipStream_t stream = hs[0]->stream;
     /* two segments whose topology pair has a fused kernel (BIOIM_FUSED_PAIRS)

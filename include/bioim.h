@@ -83,6 +83,20 @@ int bioim_reset(bioim_handle_t *h, const int32_t *env_ids, const int32_t *ref_in
  * same launch and their obs row is the post-reset observation. */
 int bioim_step(bioim_handle_t *h, const void *actions, void *obs, void *reward, uint8_t *done, void *info);
 int bioim_set_auto_reset(bioim_handle_t *h, int on);
+/* In-kernel auto-resets of a muscle model (default step kernels: no push
+ * table, semi-implicit, no force report / state storage) read the reset
+ * state and observation of the drawn reference row from a per-handle table
+ * instead of running the reset realize with fiber equilibrium in the step
+ * launch (that realize made every launch wait for its slowest wave).  The
+ * table is built once, on the first such step, by that same reset realize
+ * (one scratch env per reference row).  on = 1 (default) uses it, 0 runs the
+ * realize in the launch as before; results agree to the rounding level of
+ * the fiber-velocity root (its warm start differs).  Replaces nothing in the
+ * reference (OsimModel.reset + equilibrateMuscles per reset,
+ * opensim_wrapper.py:293-297). */
+int bioim_set_reset_table(bioim_handle_t *h, int on);
+/* rows of the handle's built reset table (0: none built yet or none wanted) */
+int bioim_reset_table_rows(const bioim_handle_t *h);
 /* Row strides (in elements) of the actions / obs / info buffers this handle
  * reads and writes (default nact, obs_dim, info_dim).  Larger strides let
  * handles of different env IDs share padded buffers. */

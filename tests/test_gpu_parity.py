@@ -744,8 +744,11 @@ def test_parity_200_steps_c3_tracking_drive():
 # fp64 -> fp32 tolerance of north_star, measured on the one drive whose fp64
 # trajectories are not chaotic (oracle twin ~1e-10 over 200 steps).  Bounds
 # per column class, relative to max(|x|, 1), over env-steps alive on both
-# sides (DESIGN.md section 2 quotes the measured values).
-FP32_FREE_TOL = {'state': None, 'rate': None, 'qdd': None, 'reward': None}
+# sides; measured worst over 200 steps (profiles/r05/r05c/tests.log): state
+# columns 2.1e-3, rate columns (speeds, fiber velocities, contact forces)
+# 9.4e-2, q'' 4.2, reward 6.4e-5.  The bounds are about
+# 2.5x the measured worst; the north_star 1e-4 holds for the reward only.
+FP32_FREE_TOL = {'state': 5e-3, 'rate': 0.25, 'qdd': 10.0, 'reward': 2e-4}
 
 
 @pytest.mark.skipif(not gpu_available(), reason='needs GPU')
@@ -825,10 +828,10 @@ def test_parity_200_steps_muscle_tracking_drive(env_id):
 
     Bounds per env and step, while the env is alive on all sides: obs and
     reward within 1e-4 relative (north_star) whenever that env's twin
-    envelope is within 1e-5 (most env-steps: the drive is not chaotic; an
-    env whose twins diverge — a rounding-level perturbation grown by contact
-    events — is held to the next bound only), and within
-    max(1e-7, 100 x its twin envelope) at every step; `done` equal; >= 50 %
+    envelope is within 1e-5, which is every env-step of every ID (asserted:
+    the drive is not chaotic on the committed schedules; the one LockedKnee3D
+    env whose twins diverged in round 4 was re-searched, tools/drive_calm.py),
+    and within max(1e-7, 100 x its twin envelope) at every step; `done` equal; >= 50 %
     of the envs survive on the oracle and on the GPU: alive at t = 200, or
     ended by the episode limit istep >= N (rows drawn near reset_hi reach it
     before t = 200; the reference's is_done, :270) without falling."""
@@ -884,7 +887,47 @@ def test_parity_200_steps_muscle_tracking_drive(env_id):
     assert (e_gpu[calm] < 1e-4).all(), np.argwhere(calm & (e_gpu >= 1e-4))[:5]
     bad = seen & (e_gpu > np.maximum(1e-7, 100 * e_twin))
     assert not bad.any(), np.argwhere(bad)[:5]
-    assert calm.sum() >= 0.9 * seen.sum(), (calm.sum(), seen.sum())
+    # every env-step calm (round 5: the one chaotic LockedKnee3D env, row 38,
+    # re-searched by tools/drive_calm.py), so north_star's 1e-4 holds on all of them
+    assert calm.sum() == seen.sum(), (calm.sum(), seen.sum())
     assert (orc_alive | limit_end).sum() >= n // 2 and (gpu_alive | limit_end).sum() >= n // 2, \
         (orc_alive.sum(), gpu_alive.sum(), limit_end.sum())
     env.close()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+@pytest.mark.parametrize('env_id', ['MuscleWalkingImitation2D-v0', 'MuscleLockedKneeImitation3D-v0'])
+def test_reset_table_matches_reset_realize(env_id):
+    """In-kernel auto-resets from the reset table (bioim_set_reset_table, the
+    default) against the reset realize run in the step launch (table off):
+    every step's state (q, u, activations, fiber lengths, counters) and
+    reward / done / info are bit-identical, and the observations agree to the
+    rounding level (a reset row's fiber velocities and q'' come from a
+    cold-started fiber-velocity root in the table); the table was built and
+    used (many resets happen), and the table-off handle never builds one."""
+    import torch
+    from bioimitation.vector_env import VectorEnv
+    n, T = 1024, 160      # fresh episodes fall from step ~50 on (the bench burns in 150 steps)
+    a = VectorEnv(env_id, n, precision=64, seed=5, auto_reset=True)
+    b = VectorEnv(env_id, n, precision=64, seed=5, auto_reset=True)
+    b.set_reset_table(False)
+    rows = np.random.default_rng(6).integers(0, a.pack.reset_hi + 1, size=n)
+    a.reset(ref_index=rows)
+    b.reset(ref_index=rows)
+    g = torch.Generator(device='cuda').manual_seed(7)
+    resets, worst = 0, 0.0
+    for t in range(T):
+        act = torch.rand((n, a.action_dim), generator=g, device=a.device, dtype=torch.float64)
+        oa, ra, da, ia = (x.clone() for x in a.step(act))
+        ob, rb, db, ib = b.step(act)
+        assert torch.equal(da, db) and torch.equal(ra, rb) and torch.equal(ia, ib), t
+        resets += int(da.sum())
+        worst = max(worst, float((oa - ob).abs().div(ob.abs().clamp(min=1.0)).max()))
+        if t % 8 == 7 or t == T - 1:
+            np.testing.assert_array_equal(a.get_state(), b.get_state())
+    assert a.reset_table_rows == a.pack.nrows and b.reset_table_rows == 0
+    assert resets > 20, resets
+    assert worst < 1e-12, worst
+    print(f'{env_id}: {resets} auto-resets over {T} steps x {n} envs; table vs realize obs max rel diff {worst:.1e}')
+    a.close()
+    b.close()
