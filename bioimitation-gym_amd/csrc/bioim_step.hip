@@ -102,6 +102,11 @@ DEV void sfor(F &&f) {
 #ifndef BIOIM_FV_PRED
 #define BIOIM_FV_PRED 0
 #endif
+/* the reset table (LaunchArgs::reset_tab) in the planar RK-Merson step
+ * kernels too (the spatial ones stay as they are: 506-512 registers) */
+#ifndef BIOIM_RESET_TAB_RK
+#define BIOIM_RESET_TAB_RK 1
+#endif
 template <typename Real> struct Eps;
 template <> struct Eps<float> {
     static constexpr float u_tol = 2e-7f;   /* Bezier parameter tolerance  */
@@ -256,6 +261,12 @@ template <int G> DEV bool group_any(bool p) {
 
 #ifdef BIOIM_STAMPS
 __device__ unsigned long long g_stamps[24];
+#endif
+/* Diagnostic build only (-DBIOIM_WAVETIME, single translation unit,
+ * tools/wavetime.py): shader cycles of every wave of the last step launch */
+#ifdef BIOIM_WAVETIME
+#define BIOIM_WAVETIME_N 65536
+__device__ unsigned long long g_wavetime[BIOIM_WAVETIME_N];
 #endif
 
 /* ------------------------------------------------------------ functions */
@@ -3174,7 +3185,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             pending_reset = true;
             do_reset = true;
             reset_row = draw_index(a.seed, a.env_offset + env, resets, M.reset_hi);
-            if constexpr (!RK && !PERT && !REP && NM > 0) {
+            if constexpr ((!RK || (BIOIM_RESET_TAB_RK && T::PLANAR)) && !PERT && !REP && NM > 0) {
                 /* the reset table (LaunchArgs::reset_tab): the state the reset
                  * realize would leave (reference row, default activation,
                  * equilibrium fiber lengths) and its observation, without a
@@ -3191,6 +3202,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                     t = M.ref_time[r];
                     istep = M.ref_istep[r];
                     has_last = 0;
+                    rk_hnext = 0;   /* reset_manager: a new integrator (opensim_wrapper.py:287-291) */
                     resets += 1;
 #pragma unroll
                     for (int j = 0; j < MPL; ++j) {
@@ -3259,7 +3271,14 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
  * untouched by it */
 template <class T, typename Real, bool PERT, bool RK, bool REP = false>
 __global__ __launch_bounds__(BIOIM_EPB * T::G) __attribute__((amdgpu_waves_per_eu(1, 1))) void env_kernel(LaunchArgs<T, Real> a) {
+#ifdef BIOIM_WAVETIME
+    const unsigned long long w0 = __builtin_amdgcn_s_memtime();
+#endif
     env_block<T, Real, PERT, RK, REP>(a, blockIdx.x);
+#ifdef BIOIM_WAVETIME
+    const unsigned w = blockIdx.x * (BIOIM_EPB * T::G / 64) + threadIdx.x / 64;
+    if ((threadIdx.x & 63) == 0 && w < BIOIM_WAVETIME_N) g_wavetime[w] = __builtin_amdgcn_s_memtime() - w0;
+#endif
 }
 
 
@@ -3712,6 +3731,7 @@ struct bioim_handle {
     const uint8_t *active; /* caller's device buffer [n] or null (bioim_set_active_mask) */
     int last_group_fused; /* the last bioim_step_group with this handle first ran one fused launch */
     void *reset_tab;      /* Real [pack.nrows][nmuscle + obs_dim] or null (build_reset_table) */
+    int planar;           /* the pack's topology is planar (pack_is_planar) */
     int reset_tab_on;     /* bioim_set_reset_table (default 1) */
     Ops ops;
     bioim_modelpack_t pack;
@@ -3721,7 +3741,8 @@ struct bioim_handle {
  * default kernels (no push table, semi-implicit) and no force report or
  * state storage (their rows come from the reset realize itself) */
 static inline bool reset_table_wanted(const bioim_handle_t *h) {
-    return h->reset_tab_on && h->auto_reset && h->nmuscle > 0 && h->pert_n == 0 && !h->rk && !h->force_out && !h->traj;
+    return h->reset_tab_on && h->auto_reset && h->nmuscle > 0 && h->pert_n == 0 && (!h->rk || (BIOIM_RESET_TAB_RK && h->planar)) &&
+           !h->force_out && !h->traj;
 }
 static inline bool reset_table_eligible(const bioim_handle_t *h) { return h->reset_tab && reset_table_wanted(h); }
 
@@ -4074,6 +4095,7 @@ int bioim_create(const bioim_modelpack_t *pack, int n_envs, int device, int prec
     h->env_offset = 0;
     h->pert_n = 0; h->pert_ob = -1;
     h->reset_tab = nullptr; h->reset_tab_on = 1;
+    h->planar = pack_is_planar(*pack) ? 1 : 0;
     h->act_stride = pack->nact; h->obs_stride = pack->obs_dim; h->info_stride = pack->info_dim;
     h->ops = ops;
     memcpy(&h->pack, pack, sizeof(bioim_modelpack_t));
@@ -4516,6 +4538,13 @@ int bioim_set_stream(bioim_handle_t *h, void *s) {
     return 0;
 }
 
+#ifdef BIOIM_WAVETIME
+int bioim_debug_wavetime(unsigned long long *out, int n) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wavetime), sizeof(unsigned long long) * (n < BIOIM_WAVETIME_N ? n : BIOIM_WAVETIME_N)));
+    return 0;
+}
+#endif
 #ifdef BIOIM_STAMPS
 int bioim_debug_stamps(unsigned long long *out, int reset) {
     HIPCHK(hipDeviceSynchronize());
