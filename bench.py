@@ -451,6 +451,12 @@ def reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist):
             'rk_budget': RK_BUDGET, 'launches': a.steps, 'ms_per_launch': t_max / a.steps * 1e3,
             'finished_env_steps': tot, 'done_rate': (sum(e.reset_count() for e in segs) - resets0) / max(local, 1),
             'evals_per_env_step': (sum(e.eval_count() for e in segs) - evals0) / max(local, 1) if counted else None,
+            # share of the launches' attempt capacity (RK_BUDGET attempts x 5 evaluations per env) that
+            # envs spent idle after finishing their step (attempt evaluations = all evaluations minus one
+            # realize per finished step and one per reset)
+            'launch_idle_share': (1.0 - (sum(e.eval_count() for e in segs) - evals0 - local -
+                                         (sum(e.reset_count() for e in segs) - resets0)) / (a.steps * n * 5 * RK_BUDGET))
+            if counted else None,
             'note': "the reference's integrator (opensim_wrapper.py:287-301) on the same workload; "
                     'GPU parity vs the oracle in tests/test_gpu_parity.py (RK) and tests/test_gpu_rk_budget.py'}
     env.close()
