@@ -102,6 +102,11 @@ DEV void sfor(F &&f) {
 #ifndef BIOIM_FV_PRED
 #define BIOIM_FV_PRED 0
 #endif
+/* solve_fv: a lane whose root lies past the curve's end leaves the Newton
+ * loop after one step (0: it iterates to the segment end as before) */
+#ifndef BIOIM_FV_PAST_END
+#define BIOIM_FV_PAST_END 1
+#endif
 /* the reset table (LaunchArgs::reset_tab) in the planar RK-Merson step
  * kernels too (the spatial ones stay as they are: 506-512 registers) */
 #ifndef BIOIM_RESET_TAB_RK
@@ -267,6 +272,10 @@ __device__ unsigned long long g_stamps[24];
 #ifdef BIOIM_WAVETIME
 #define BIOIM_WAVETIME_N 65536
 __device__ unsigned long long g_wavetime[BIOIM_WAVETIME_N];
+/* per thread of the last launch: fiber-velocity Newton iterations (sum over
+ * the launch's solves), the most of one solve, bisection fallbacks */
+__device__ unsigned g_fvit[BIOIM_WAVETIME_N * 4], g_fvmax[BIOIM_WAVETIME_N * 4], g_fvbis[BIOIM_WAVETIME_N * 4];
+DEV unsigned diag_tid() { return blockIdx.x * blockDim.x + threadIdx.x; }
 #endif
 
 /* ------------------------------------------------------------ functions */
@@ -514,7 +523,7 @@ DEV void curve_eval(const DCurve<Real> &C, Real x, Real &y, Real &dydx) {
  * previous substep's root) through the segment's u(x) table; returns v, fv,
  * dfv/dv.  At least two safeguarded Newton steps, then more until
  * converged. */
-template <bool BF = true, typename Real>
+template <bool BF = true, bool PE = true, typename Real>
 DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0, Real &v, Real &fv, Real &dfv) {
     Real g0 = afal * C.y0 + beta * C.x0 - rhs;
     Real g1 = afal * C.y1 + beta * C.x1 - rhs;
@@ -565,6 +574,16 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
     for (int i = 0; i < 6; ++i) pg[i] = afal * py[i] + beta * px[i];
     pg[0] -= rhs;
     Real lo = 0, hi = 1, dprev = 1;
+    /* the root lies past an end of the curve (g keeps one sign over it): the
+     * result is the linear extrapolation below, whatever the loop finds, so
+     * the lane leaves the loop after its first step.  Before round 5 such a
+     * lane ran the Newton loop down to the segment's end by bisections (up to
+     * ~40 iterations) and its wave — and the launch — waited for it: the
+     * raw-action Palsy3D model hit it in 10 % of its waves.
+     * PE: the spatial models only (same-box Palsy3D -15 %, C5 -13 %,
+     * Running3D -1.5 %; the planar kernels, which rarely meet it, measured
+     * +0.5 % with it: profiles/r05/r05k) */
+    const bool past_end = PE && BIOIM_FV_PAST_END && ((g0 >= 0) | (g1 <= 0));
     for (int it = 0; it < Eps<Real>::it_max; ++it) {
         Real g = bez5(pg, u);
         if (g > 0) hi = u; else lo = u;
@@ -573,10 +592,19 @@ DEV void solve_fv(const DCurve<Real> &C, Real afal, Real beta, Real rhs, Real v0
         /* inclusive bracket: a converged step (un == u == lo or hi after
          * rounding) must not trigger the bisection fallback */
         if (!(un >= lo && un <= hi)) un = Real(0.5) * (lo + hi);
+#ifdef BIOIM_WAVETIME
+        if (!(u - g * newton_rcp(dg) >= lo && u - g * newton_rcp(dg) <= hi) && diag_tid() < BIOIM_WAVETIME_N * 4) g_fvbis[diag_tid()] += 1;
+#endif
         Real du = fabs(un - u);
         u = un;
         /* converged, or stagnating at the rounding level of g */
-        if (it >= 1 && (du <= Eps<Real>::u_stop || (du <= Real(1e3) * Eps<Real>::u_tol && du >= Real(0.5) * dprev))) {
+        if (past_end || (it >= 1 && (du <= Eps<Real>::u_stop || (du <= Real(1e3) * Eps<Real>::u_tol && du >= Real(0.5) * dprev)))) {
+#ifdef BIOIM_WAVETIME
+            if (diag_tid() < BIOIM_WAVETIME_N * 4) {
+                g_fvit[diag_tid()] += it + 1;
+                if ((unsigned)(it + 1) > g_fvmax[diag_tid()]) g_fvmax[diag_tid()] = it + 1;
+            }
+#endif
 #ifdef BIOIM_STAMPS
             if (blockIdx.x == 0 && threadIdx.x < 14) atomicAdd(&g_stamps[12], (unsigned long long)(it + 1));
             if (blockIdx.x == 0 && threadIdx.x < 14) atomicAdd(&g_stamps[13], 1ull);
@@ -1405,7 +1433,7 @@ DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_
     Real rhs = fse * icos - fpe;
     STAMP(16);
     Real vN, fvv, dfv;
-    solve_fv<BFC>(Cfv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
+    solve_fv<BFC, !T::PLANAR>(Cfv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
     STAMP(17);
     Real dGdv = a * fal * dfv + mu.beta;
     /* selects over plain locals (a load in a ?: arm or an if body becomes a
@@ -3273,6 +3301,7 @@ template <class T, typename Real, bool PERT, bool RK, bool REP = false>
 __global__ __launch_bounds__(BIOIM_EPB * T::G) __attribute__((amdgpu_waves_per_eu(1, 1))) void env_kernel(LaunchArgs<T, Real> a) {
 #ifdef BIOIM_WAVETIME
     const unsigned long long w0 = __builtin_amdgcn_s_memtime();
+    if (diag_tid() < BIOIM_WAVETIME_N * 4) { g_fvit[diag_tid()] = 0; g_fvmax[diag_tid()] = 0; g_fvbis[diag_tid()] = 0; }
 #endif
     env_block<T, Real, PERT, RK, REP>(a, blockIdx.x);
 #ifdef BIOIM_WAVETIME
@@ -4542,6 +4571,15 @@ int bioim_set_stream(bioim_handle_t *h, void *s) {
 int bioim_debug_wavetime(unsigned long long *out, int n) {
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wavetime), sizeof(unsigned long long) * (n < BIOIM_WAVETIME_N ? n : BIOIM_WAVETIME_N)));
+    return 0;
+}
+/* per thread: [0, n) Newton iterations, [n, 2n) most in one solve, [2n, 3n) bisections */
+int bioim_debug_fviter(unsigned *out, int n) {
+    HIPCHK(hipDeviceSynchronize());
+    const int m = n < BIOIM_WAVETIME_N * 4 ? n : BIOIM_WAVETIME_N * 4;
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fvit), sizeof(unsigned) * m));
+    HIPCHK(hipMemcpyFromSymbol(out + n, HIP_SYMBOL(g_fvmax), sizeof(unsigned) * m));
+    HIPCHK(hipMemcpyFromSymbol(out + 2 * n, HIP_SYMBOL(g_fvbis), sizeof(unsigned) * m));
     return 0;
 }
 #endif

@@ -43,6 +43,12 @@ for k in range(150):
     env.step(acts[k % 64])
 nw = env.launch['workgroups'] * env.launch['threads_per_workgroup'] // 64
 buf = (C.c_ulonglong * nw)()
+fvf = getattr(L, 'bioim_debug_fviter', None)
+nt = nw * 64
+fvb = (C.c_uint * (3 * nt))()
+if fvf is not None:
+    fvf.argtypes = [C.POINTER(C.c_uint), C.c_int]
+fv_rows = []
 rows = []
 raw = []
 for k in range(20):
@@ -51,8 +57,22 @@ for k in range(20):
     f(buf, nw)
     d = np.array(buf[:], dtype=np.float64)
     raw.append([d])
+    if fvf is not None:
+        fvf(fvb, nt)
+        it = np.array(fvb[:nt], dtype=np.float64).reshape(nw, 64)
+        mx = np.array(fvb[nt:2 * nt], dtype=np.float64).reshape(nw, 64)
+        bi = np.array(fvb[2 * nt:], dtype=np.float64).reshape(nw, 64)
+        fv_rows.append((d, it.max(1), mx.max(1), bi.sum(1)))
     rows.append((d.mean(), np.median(d), np.percentile(d, 90), np.percentile(d, 99), d.max(), int(env.done.sum())))
 a = np.array(rows)
+if fv_rows:
+    d = np.concatenate([r[0] for r in fv_rows]); itm = np.concatenate([r[1] for r in fv_rows])
+    mxm = np.concatenate([r[2] for r in fv_rows]); bis = np.concatenate([r[3] for r in fv_rows])
+    slow = d > np.percentile(d, 90)
+    print(f'  fiber-velocity Newton per wave (max over its lanes of the launch total / of one solve; bisections): '
+          f'all waves {itm.mean():.1f} / {mxm.mean():.1f}; {bis.mean():.2f};  slowest 10 % {itm[slow].mean():.1f} / '
+          f'{mxm[slow].mean():.1f}; {bis[slow].mean():.2f};  corr(cycles, lane-max total) {np.corrcoef(d, itm)[0, 1]:.2f}, '
+          f'corr(cycles, bisections) {np.corrcoef(d, bis)[0, 1]:.2f}')
 out = os.environ.get('WAVETIME_OUT')
 if out:   # raw per-wave cycles of the 20 launches, for offline analysis
     np.save(out, np.array([r[0] for r in raw]))
