@@ -3213,12 +3213,14 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             pending_reset = true;
             do_reset = true;
             reset_row = draw_index(a.seed, a.env_offset + env, resets, M.reset_hi);
-            if constexpr ((!RK || (BIOIM_RESET_TAB_RK && T::PLANAR)) && !PERT && !REP && NM > 0) {
+            if constexpr ((!RK || (BIOIM_RESET_TAB_RK && T::PLANAR)) && !PERT && !REP) {
                 /* the reset table (LaunchArgs::reset_tab): the state the reset
                  * realize would leave (reference row, default activation,
                  * equilibrium fiber lengths) and its observation, without a
                  * dynamics call and fiber equilibrium in this wave — they made
-                 * the launch wait for its slowest wave */
+                 * the launch wait for its slowest wave.  Torque
+                 * models: the observation's q'' holds the held torques, so the
+                 * row carries M^-1 too and q''_d = q''_d(0) + (M^-1 tau)_d */
                 if (a.reset_tab) {
                     const int r = clamp_row(reset_row, M.nrows);
                     const Real *tr = a.reset_tab + (size_t)r * a.reset_tab_dim;
@@ -3232,14 +3234,49 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                     has_last = 0;
                     rk_hnext = 0;   /* reset_manager: a new integrator (opensim_wrapper.py:287-291) */
                     resets += 1;
+                    if constexpr (NM > 0) {
 #pragma unroll
-                    for (int j = 0; j < MPL; ++j) {
-                        const int m = mslot<T>(lane + j * G);
-                        if (m < NM) { act[j] = SM.mus[m].default_act; lce[j] = tr[m]; }
+                        for (int j = 0; j < MPL; ++j) {
+                            const int m = mslot<T>(lane + j * G);
+                            if (m < NM) { act[j] = SM.mus[m].default_act; lce[j] = tr[m]; }
+                        }
+                        if (obs)
+                            for (int k = lane; k < M.obs_dim; k += G)
+                                GAT(obs, (size_t)env * a.obs_stride + k, (size_t)N * a.obs_stride) = tr[NM + k];
+                    } else {
+                        /* the held torques per dof, gathered as in the dynamics
+                         * call (TAU slots, SM.tau_src), then q'' per dof lane */
+                        constexpr int NI = ND * ND;
+                        if (lane == 0) lds[LY::TAU + LY::TZ] = Real(0);
+#pragma unroll
+                        for (int j = 0; j < MPL; ++j) {
+                            const int m = mslot<T>(lane + j * G);
+                            if (m < NA) lds[LY::TAU + (lane + j * G) * T::MAXSPAN] = control[j] * SM.ca_opt[m];
+                        }
+                        wave_sync();
+                        if (lane < ND) {
+                            Real tau = 0;
+#pragma unroll
+                            for (int i = 0; i < T::MAXARM; ++i) tau += lds[LY::TAU + SM.tau_src[lane][i]];
+                            lds[LY::RHS + lane] = tau;
+                        }
+                        wave_sync();
+                        Real *ob = lds + LY::OBS;
+                        for (int k = lane; k < M.obs_dim; k += G) ob[k] = tr[NI + k];
+                        wave_sync();
+                        if (lane < ND) {
+                            using OL = ObsLayout<T>;
+                            const int c = SM.dof_coord[lane];
+                            Real x = ob[OL::QACC + c];
+#pragma unroll
+                            for (int k = 0; k < ND; ++k) x = fma(tr[lane * ND + k], lds[LY::RHS + k], x);
+                            ob[OL::QACC + c] = x;
+                        }
+                        wave_sync();
+                        if (obs)
+                            for (int k = lane; k < M.obs_dim; k += G)
+                                GAT(obs, (size_t)env * a.obs_stride + k, (size_t)N * a.obs_stride) = ob[k];
                     }
-                    if (obs)
-                        for (int k = lane; k < M.obs_dim; k += G)
-                            GAT(obs, (size_t)env * a.obs_stride + k, (size_t)N * a.obs_stride) = tr[NM + k];
                     break;
                 }
             }
@@ -3759,7 +3796,7 @@ struct bioim_handle {
     uint8_t *ready_out; /* caller's device buffer [n] or null */
     const uint8_t *active; /* caller's device buffer [n] or null (bioim_set_active_mask) */
     int last_group_fused; /* the last bioim_step_group with this handle first ran one fused launch */
-    void *reset_tab;      /* Real [pack.nrows][nmuscle + obs_dim] or null (build_reset_table) */
+    void *reset_tab;      /* Real [pack.nrows][reset_table_dim] or null (build_reset_table) */
     int planar;           /* the pack's topology is planar (pack_is_planar) */
     int reset_tab_on;     /* bioim_set_reset_table (default 1) */
     Ops ops;
@@ -3770,10 +3807,15 @@ struct bioim_handle {
  * default kernels (no push table, semi-implicit) and no force report or
  * state storage (their rows come from the reset realize itself) */
 static inline bool reset_table_wanted(const bioim_handle_t *h) {
-    return h->reset_tab_on && h->auto_reset && h->nmuscle > 0 && h->pert_n == 0 && (!h->rk || (BIOIM_RESET_TAB_RK && h->planar)) &&
+    return h->reset_tab_on && h->auto_reset && h->pert_n == 0 && (!h->rk || (BIOIM_RESET_TAB_RK && h->planar)) &&
            !h->force_out && !h->traj;
 }
 static inline bool reset_table_eligible(const bioim_handle_t *h) { return h->reset_tab && reset_table_wanted(h); }
+/* reals per table row: muscle models [nmuscle fiber lengths][obs]; torque
+ * models [ndof x ndof M^-1, row-major][obs at zero held torques] */
+static inline int reset_table_dim(const bioim_handle_t *h) {
+    return (h->nmuscle > 0 ? h->nmuscle : h->ndof * h->ndof) + h->obs_dim;
+}
 
 namespace {
 
@@ -3827,7 +3869,7 @@ LaunchArgs<T, Real> make_args(bioim_handle_t *h, int mode, const void *actions, 
     a.controls_in = oc ? reinterpret_cast<const Real *>(oc->controls) : nullptr;
     a.osim_out = oc ? reinterpret_cast<Real *>(oc->report) : nullptr;
     a.reset_tab = mode == 0 && reset_table_eligible(h) ? reinterpret_cast<const Real *>(h->reset_tab) : nullptr;
-    a.reset_tab_dim = h->nmuscle + h->obs_dim;
+    a.reset_tab_dim = reset_table_dim(h);
     return a;
 }
 
@@ -4176,30 +4218,37 @@ int bioim_reset(bioim_handle_t *h, const int32_t *env_ids, const int32_t *ref_in
     return 0;
 }
 
-/* The reset table of a muscle-model handle (LaunchArgs::reset_tab), built
- * once, on the first step that can use it: a scratch handle of the same pack
- * and precision with one env per reference row is reset to row r (mode 1 —
- * the very reset realize with fiber equilibrium an auto-reset runs), and its
- * fiber lengths and observations are kept.  A reset realize depends on the
- * row alone for these models: the held excitations enter only the activation
- * rate, which the observation does not hold; the fiber-velocity root differs
- * from a warm-started one at the rounding level only (its start is cold). */
+/* The reset table of a handle (LaunchArgs::reset_tab), built once, on the
+ * first step that can use it: a scratch handle of the same pack and precision
+ * with one env per reference row is reset to row r (mode 1 — the very reset
+ * realize, with fiber equilibrium, an auto-reset runs) and its observations
+ * are kept.  Muscle models: with the equilibrium fiber lengths; the reset
+ * realize depends on the row alone (the held excitations enter only the
+ * activation rate, which the observation does not hold; the fiber-velocity
+ * root differs from a warm-started one at the rounding level: its start is
+ * cold).  Torque models: the held torques enter the observation's q'' only,
+ * linearly (q'' = M^-1 (f + tau)), so the row keeps q'' at zero torque (the
+ * scratch handle's held controls are 0) and M^-1 at the row's coordinates. */
 static int build_reset_table(bioim_handle_t *h) {
     const int nr = h->pack.nrows, nm = h->nmuscle, od = h->obs_dim, nd = h->ndof;
-    const size_t R = h->precision == 64 ? 8 : 4, dim = (size_t)nm + od;
+    const size_t R = h->precision == 64 ? 8 : 4, head = nm > 0 ? (size_t)nm : (size_t)nd * nd, dim = head + od;
     bioim_handle_t *tmp = nullptr;
     int rc = bioim_create(&h->pack, nr, h->device, h->precision, h->seed, &tmp);
     if (rc) return rc;
     int32_t *d_idx = nullptr;
-    void *d_obs = nullptr, *d_tab = nullptr;
+    void *d_obs = nullptr, *d_tab = nullptr, *d_q = nullptr, *d_v = nullptr, *d_out = nullptr;
     std::vector<int32_t> idx(nr);
     for (int r = 0; r < nr; ++r) idx[r] = r;
     const int sdim = bioim_state_dim(tmp);
     std::vector<double> st((size_t)nr * sdim);
     std::vector<unsigned char> obs((size_t)nr * od * R), tab((size_t)nr * dim * R);
+    auto put = [&](unsigned char *dst, double x) {
+        if (R == 8) memcpy(dst, &x, 8);
+        else { const float f = (float)x; memcpy(dst, &f, 4); }
+    };
     auto done = [&](int code) {
-        if (d_idx) hipFree(d_idx);
-        if (d_obs) hipFree(d_obs);
+        for (void *p : {(void *)d_idx, d_obs, d_q, d_v, d_out})
+            if (p) hipFree(p);
         if (code && d_tab) hipFree(d_tab);
         bioim_destroy(tmp);
         return code;
@@ -4213,15 +4262,39 @@ static int build_reset_table(bioim_handle_t *h) {
         hipMemcpy(obs.data(), d_obs, obs.size(), hipMemcpyDeviceToHost) != hipSuccess)
         return done(fail(BIOIM_E_DEVICE, "build_reset_table: reset realize failed"));
     if ((rc = bioim_get_state(tmp, st.data())) != 0) return done(rc);
-    for (int r = 0; r < nr; ++r) {
-        unsigned char *row = tab.data() + (size_t)r * dim * R;
-        for (int m = 0; m < nm; ++m) {
-            const double l = st[(size_t)r * sdim + 5 + 2 * nd + nm + m];   /* fiber_length[m] */
-            if (R == 8) memcpy(row + m * R, &l, 8);
-            else { const float f = (float)l; memcpy(row + m * R, &f, 4); }
-        }
-        memcpy(row + (size_t)nm * R, obs.data() + (size_t)r * od * R, (size_t)od * R);
+    if (nm > 0) {
+        for (int r = 0; r < nr; ++r)
+            for (int m = 0; m < nm; ++m)   /* fiber_length[m] */
+                put(tab.data() + ((size_t)r * dim + m) * R, st[(size_t)r * sdim + 5 + 2 * nd + nm + m]);
+    } else {
+        /* torque models: M^-1 at each row's coordinates, column k = M^-1 e_k
+         * (the inverse-dynamics kernel, BIOIM_ID_MULT_MINV: the realize's
+         * mass matrix — at h = 0 no implicit contact or limit terms) */
+        const size_t n = (size_t)nr * nd;
+        std::vector<unsigned char> q(n * nd * R), v(n * nd * R, 0), out(n * nd * R);
+        for (int r = 0; r < nr; ++r)
+            for (int k = 0; k < nd; ++k) {
+                const size_t s_ = (size_t)r * nd + k;   /* state: row r, unit vector e_k */
+                for (int d = 0; d < nd; ++d) put(q.data() + (s_ * nd + d) * R, st[(size_t)r * sdim + 5 + d]);
+                put(v.data() + (s_ * nd + k) * R, 1.0);
+            }
+        if (hipMalloc(&d_q, q.size()) != hipSuccess || hipMalloc(&d_v, v.size()) != hipSuccess ||
+            hipMalloc(&d_out, out.size()) != hipSuccess ||
+            hipMemcpy(d_q, q.data(), q.size(), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(d_v, v.data(), v.size(), hipMemcpyHostToDevice) != hipSuccess)
+            return done(fail(BIOIM_E_DEVICE, "build_reset_table: allocation failed"));
+        if ((rc = bioim_id_eval(tmp, BIOIM_ID_MULT_MINV, (int)n, d_q, d_q, d_v, d_out)) != 0) return done(rc);
+        if (hipStreamSynchronize(tmp->stream) != hipSuccess ||
+            hipMemcpy(out.data(), d_out, out.size(), hipMemcpyDeviceToHost) != hipSuccess)
+            return done(fail(BIOIM_E_DEVICE, "build_reset_table: M^-1 columns failed"));
+        for (int r = 0; r < nr; ++r)
+            for (int k = 0; k < nd; ++k)
+                for (int d = 0; d < nd; ++d)   /* M^-1[d][k] = (M^-1 e_k)_d, row-major */
+                    memcpy(tab.data() + ((size_t)r * dim + (size_t)d * nd + k) * R,
+                           out.data() + (((size_t)r * nd + k) * nd + d) * R, R);
     }
+    for (int r = 0; r < nr; ++r)
+        memcpy(tab.data() + ((size_t)r * dim + head) * R, obs.data() + (size_t)r * od * R, (size_t)od * R);
     if (hipMemcpy(d_tab, tab.data(), tab.size(), hipMemcpyHostToDevice) != hipSuccess)
         return done(fail(BIOIM_E_DEVICE, "build_reset_table: upload failed"));
     h->reset_tab = d_tab;

@@ -83,9 +83,10 @@ int bioim_reset(bioim_handle_t *h, const int32_t *env_ids, const int32_t *ref_in
  * same launch and their obs row is the post-reset observation. */
 int bioim_step(bioim_handle_t *h, const void *actions, void *obs, void *reward, uint8_t *done, void *info);
 int bioim_set_auto_reset(bioim_handle_t *h, int on);
-/* In-kernel auto-resets of a muscle model (default step kernels: no push
- * table, semi-implicit, no force report / state storage) read the reset
- * state and observation of the drawn reference row from a per-handle table
+/* In-kernel auto-resets (default step kernels: no push table, semi-implicit
+ * or planar RK-Merson, no force report / state storage) read the reset state
+ * and observation of the drawn reference row from a per-handle table (torque
+ * models: with M^-1 at the row, for the held torques' share of q'')
  * instead of running the reset realize with fiber equilibrium in the step
  * launch (that realize made every launch wait for its slowest wave).  The
  * table is built once, on the first such step, by that same reset realize

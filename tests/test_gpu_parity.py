@@ -898,7 +898,9 @@ def test_parity_200_steps_muscle_tracking_drive(env_id):
 @pytest.mark.skipif(not gpu_available(), reason='needs GPU')
 @pytest.mark.parametrize('env_id,integrator', [('MuscleWalkingImitation2D-v0', 'semi-implicit'),
                                                ('MuscleLockedKneeImitation3D-v0', 'semi-implicit'),
-                                               ('MuscleWalkingImitation2D-v0', 'rk-merson')])
+                                               ('MuscleWalkingImitation2D-v0', 'rk-merson'),
+                                               ('TorqueWalkingImitation2D-v0', 'semi-implicit'),
+                                               ('TorqueWalkingImitation3D-v0', 'semi-implicit')])
 def test_reset_table_matches_reset_realize(env_id, integrator):
     """In-kernel auto-resets from the reset table (bioim_set_reset_table, the
     default) against the reset realize run in the step launch (table off):
@@ -918,9 +920,16 @@ def test_reset_table_matches_reset_realize(env_id, integrator):
     a.reset(ref_index=rows)
     b.reset(ref_index=rows)
     g = torch.Generator(device='cuda').manual_seed(7)
+    pk = a.pack
     resets, worst = 0, 0.0
     for t in range(T):
-        act = torch.rand((n, a.action_dim), generator=g, device=a.device, dtype=torch.float64)
+        if pk.nmuscle:
+            act = torch.rand((n, a.action_dim), generator=g, device=a.device, dtype=torch.float64)
+        else:   # PD targets: the reference row's joint angles + noise (the torque models' drive)
+            st = a.get_state()[:, 1].astype(int) + 1
+            base = np.array([[pk.ref_q[min(r, pk.nrows - 1)][pk.pd_coord[i]] for i in range(a.action_dim)] for r in st])
+            act = torch.as_tensor(base, device=a.device) + 0.3 * torch.randn((n, a.action_dim), generator=g,
+                                                                            device=a.device, dtype=torch.float64)
         oa, ra, da, ia = (x.clone() for x in a.step(act))
         ob, rb, db, ib = b.step(act)
         assert torch.equal(da, db) and torch.equal(ra, rb) and torch.equal(ia, ib), t
@@ -930,7 +939,9 @@ def test_reset_table_matches_reset_realize(env_id, integrator):
             np.testing.assert_array_equal(a.get_state(), b.get_state())
     assert a.reset_table_rows == a.pack.nrows and b.reset_table_rows == 0
     assert resets > 20, resets
-    assert worst < 1e-10, worst      # observed 4.1e-12 (q'' of reset rows: the fiber-velocity root's last bits)
+    # observed 4.1e-12 (q'' of reset rows: the fiber-velocity root's last bits; torque models: M^-1 tau
+    # from the inverse-dynamics kernel's M against the realize's factorization)
+    assert worst < 1e-10, worst
     print(f'{env_id} {integrator}: {resets} auto-resets over {T} steps x {n} envs; table vs realize obs max rel diff {worst:.1e}')
     a.close()
     b.close()
