@@ -932,9 +932,12 @@ def test_reset_table_matches_reset_realize(env_id, integrator):
                                                                             device=a.device, dtype=torch.float64)
         oa, ra, da, ia = (x.clone() for x in a.step(act))
         ob, rb, db, ib = b.step(act)
-        assert torch.equal(da, db) and torch.equal(ra, rb) and torch.equal(ia, ib), t
+        # bit-equal, NaN equal to NaN (a torque env driven to a non-finite state ends with NaN outputs on both)
+        same = lambda x, y: bool(((x == y) | (x.isnan() & y.isnan())).all()) if x.is_floating_point() else torch.equal(x, y)
+        assert same(da, db) and same(ra, rb) and same(ia, ib), t
         resets += int(da.sum())
-        worst = max(worst, float((oa - ob).abs().div(ob.abs().clamp(min=1.0)).max()))
+        worst = max(worst, float(torch.nan_to_num((oa - ob).abs().div(ob.abs().clamp(min=1.0)), nan=0.0).max()))
+        assert bool((oa.isnan() == ob.isnan()).all()), t
         if t % 8 == 7 or t == T - 1:
             np.testing.assert_array_equal(a.get_state(), b.get_state())
     assert a.reset_table_rows == a.pack.nrows and b.reset_table_rows == 0
