@@ -102,6 +102,15 @@ DEV void sfor(F &&f) {
 #ifndef BIOIM_FV_PRED
 #define BIOIM_FV_PRED 0
 #endif
+/* the substep's fiber-length update through fast_rcp (0: IEEE division) */
+#ifndef BIOIM_SUBSTEP_RCP
+#define BIOIM_SUBSTEP_RCP 1
+#endif
+/* BIOIM_SGB: sched_group_barrier pipelines in the muscle eval (round-5
+ * experiment, off; same box C3 +1.3 % / +1.8 %: profiles/r05/r05o) */
+#ifndef BIOIM_SGB
+#define BIOIM_SGB 0
+#endif
 /* solve_fv: a lane whose root lies past the curve's end leaves the Newton
  * loop after one step (0: it iterates to the segment end as before) */
 #ifndef BIOIM_FV_PAST_END
@@ -1430,6 +1439,21 @@ DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_
     curve_eval<BFC>(Cfse, lt * mu.inv_lts, fse, dfse);
     curve_eval<BFC>(Cfal, lce * mu.inv_lopt, fal, dfal);
     curve_eval<BFC>(Cfpe, lce * mu.inv_lopt, fpe, dfpe);
+#if BIOIM_SGB == 1
+    /* round-5 scheduling experiment: a pipeline that issues
+     * the curves' LDS reads in groups ahead of VALU work of this block */
+#pragma unroll
+    for (int gI = 0; gI < 6; ++gI) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);   /* DS reads */
+        __builtin_amdgcn_sched_group_barrier(0x2, 12, 0);    /* VALU */
+    }
+#elif BIOIM_SGB == 2
+#pragma unroll
+    for (int gI = 0; gI < 24; ++gI) {
+        __builtin_amdgcn_sched_group_barrier(0x2, 3, 0);     /* VALU */
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   /* DS read */
+    }
+#endif
     Real rhs = fse * icos - fpe;
     STAMP(16);
     Real vN, fvv, dfv;
@@ -2959,7 +2983,14 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                     if (m < NM) {
                         act[j] += dt * D.ms[j].dadt;
                         if (!D.ms[j].clamped) {
+#if BIOIM_SUBSTEP_RCP
+                            /* a refined hardware reciprocal (fast_rcp) instead of the IEEE
+                             * division: the divisor 1 - dt dv/dl is a well-scaled positive
+                             * quantity; once per muscle and substep */
+                            Real ln = lce[j] + dt * D.ms[j].vce * fast_rcp(Real(1) - dt * D.ms[j].dvdl);
+#else
                             Real ln = lce[j] + dt * D.ms[j].vce / (Real(1) - dt * D.ms[j].dvdl);
+#endif
                             lce[j] = ln < SM.mus[m].lmin ? SM.mus[m].lmin : ln;
                         }
                     }
