@@ -102,9 +102,12 @@ DEV void sfor(F &&f) {
 #ifndef BIOIM_FV_PRED
 #define BIOIM_FV_PRED 0
 #endif
-/* the substep's fiber-length update through fast_rcp (0: IEEE division) */
+/* the substep's fiber-length update through fast_rcp instead of the IEEE
+ * division (round-5 experiment, off: the oracle divides, and after 6 steps
+ * the realize report drifted to 1.4e-9 of it, past the 1e-9 report test,
+ * profiles/r05/r05p/gpu_tests.log) */
 #ifndef BIOIM_SUBSTEP_RCP
-#define BIOIM_SUBSTEP_RCP 1
+#define BIOIM_SUBSTEP_RCP 0
 #endif
 /* BIOIM_SGB: sched_group_barrier pipelines in the muscle eval (round-5
  * experiment, off; same box C3 +1.3 % / +1.8 %: profiles/r05/r05o) */
