@@ -90,7 +90,8 @@ int bioim_set_auto_reset(bioim_handle_t *h, int on);
  * instead of running the reset realize with fiber equilibrium in the step
  * launch (that realize made every launch wait for its slowest wave).  The
  * table is built once, on the first such step, by that same reset realize
- * (one scratch env per reference row).  on = 1 (default) uses it, 0 runs the
+ * (one scratch env per reference row); that step blocks while it is built
+ * (milliseconds).  on = 1 (default) uses it, 0 runs the
  * realize in the launch as before; results agree to the rounding level of
  * the fiber-velocity root (its warm start differs).  Replaces nothing in the
  * reference (OsimModel.reset + equilibrateMuscles per reset,
