@@ -119,6 +119,9 @@ DEV void sfor(F &&f) {
 #ifndef BIOIM_FV_PAST_END
 #define BIOIM_FV_PAST_END 1
 #endif
+#ifndef BIOIM_FV_PE_PLANAR
+#define BIOIM_FV_PE_PLANAR 0
+#endif
 /* the reset table (LaunchArgs::reset_tab) in the planar RK-Merson step
  * kernels too (the spatial ones stay as they are: 506-512 registers) */
 #ifndef BIOIM_RESET_TAB_RK
@@ -1460,7 +1463,7 @@ DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_
     Real rhs = fse * icos - fpe;
     STAMP(16);
     Real vN, fvv, dfv;
-    solve_fv<BFC, !T::PLANAR>(Cfv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
+    solve_fv<BFC, !T::PLANAR || BIOIM_FV_PE_PLANAR>(Cfv, a * fal, mu.beta, rhs, v_warm, vN, fvv, dfv);
     STAMP(17);
     Real dGdv = a * fal * dfv + mu.beta;
     /* selects over plain locals (a load in a ?: arm or an if body becomes a
