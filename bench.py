@@ -293,14 +293,13 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         dist.barrier()
+    # budgeted RK: envs whose step finished, from the launches' own counter (bioim_finished_count)
+    fin0 = env.finished_count() if a.rk_budget else 0
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    finished = torch.zeros(n, dtype=torch.int32, device=dev) if a.rk_budget else None
     ev0.record(stream)
     for k in range(a.steps):
         env.step(acts[(k0 + k) % pool])
-        if finished is not None:
-            finished += env.ready   # envs whose step finished in this launch (one small add per launch)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
@@ -312,7 +311,7 @@ def main():
         tt = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt[0])
-    steps_local = int(finished.sum()) if finished is not None else n * a.steps
+    steps_local = env.finished_count() - fin0 if a.rk_budget else n * a.steps
     if dist:
         st_ = torch.tensor([steps_local], dtype=torch.float64)
         dist.all_reduce(st_)
@@ -426,6 +425,10 @@ def reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist):
     resets0 = sum(e.reset_count() for e in segs)
     counted = hasattr(segs[0]._L, 'bioim_eval_count')    # older A/B builds lack the counter
     evals0 = sum(e.eval_count() for e in segs) if counted else 0
+    # finished steps from the launches' own per-env counter (bioim_finished_count), so the timed
+    # region holds the step launches only (summing ready[] after each launch cost 1 % on C3)
+    in_kernel = hasattr(segs[0]._L, 'bioim_finished_count')
+    fin0 = sum(e.finished_count() for e in segs) if in_kernel else 0
     fin.zero_()
     if dist:
         dist.barrier()
@@ -433,12 +436,13 @@ def reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist):
     t0 = time.perf_counter()
     for k in range(a.steps):
         env.step(acts[(k0 + k) % pool])
-        count_ready()
+        if not in_kernel:
+            count_ready()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     if dist:
         dist.barrier()
-    local = int(fin.sum())
+    local = sum(e.finished_count() for e in segs) - fin0 if in_kernel else int(fin.sum())
     tot, t_max = float(local), wall
     if dist:
         tt = torch.tensor([wall], dtype=torch.float64)

@@ -18,7 +18,8 @@ LIB_PATH = os.environ.get('BIOIM_LIB', os.path.join(PKG_ROOT, 'build', 'libbioim
 EXPORTS = ['bioim_create', 'bioim_destroy', 'bioim_reset', 'bioim_step', 'bioim_set_auto_reset', 'bioim_set_env_offset', 'bioim_set_io_strides', 'bioim_step_group', 'bioim_set_group_fusion', 'bioim_group_fused', 'bioim_set_reset_table', 'bioim_reset_table_rows', 'bioim_set_perturbation', 'bioim_id_eval', 'bioim_state_dim',
            'bioim_get_state', 'bioim_set_state', 'bioim_query', 'bioim_query_launch', 'bioim_stream', 'bioim_set_stream', 'bioim_sync',
            'bioim_last_error', 'bioim_modelpack_size', 'bioim_build_id', 'bioim_reset_count', 'bioim_set_final_obs', 'bioim_set_integrator', 'bioim_force_report_dim', 'bioim_set_force_report',
-           'bioim_set_rk_budget', 'bioim_pending_count', 'bioim_set_active_mask', 'bioim_osim', 'bioim_osim_report_dim', 'bioim_eval_count', 'bioim_set_state_storage']
+           'bioim_set_rk_budget', 'bioim_pending_count', 'bioim_set_active_mask', 'bioim_osim', 'bioim_osim_report_dim', 'bioim_eval_count', 'bioim_set_state_storage',
+           'bioim_finished_count']
 
 _lib = None
 
@@ -72,6 +73,7 @@ def load():
         'bioim_osim': (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, vp]),
         'bioim_osim_report_dim': (C.c_int, [vp]),
         'bioim_eval_count': (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+        'bioim_finished_count': (C.c_int, [vp, C.POINTER(C.c_uint64)]),
         'bioim_set_state_storage': (C.c_int, [vp, vp, C.c_int, vp]),
     }
     for name, (res, args) in sig.items():

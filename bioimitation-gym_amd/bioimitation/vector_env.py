@@ -311,6 +311,13 @@ class VectorEnv:
         _lib.check(self._L.bioim_eval_count(self._h, C.byref(n)))
         return int(n.value)
 
+    def finished_count(self) -> int:
+        """Env steps the adaptive integrator finished so far over all envs
+        (bioim_finished_count: the rows whose ``ready`` was 1)."""
+        n = C.c_uint64()
+        _lib.check(self._L.bioim_finished_count(self._h, C.byref(n)))
+        return int(n.value)
+
     def sync(self):
         _lib.check(self._L.bioim_sync(self._h))
 

@@ -241,5 +241,8 @@ struct DState {
     int32_t *rka;   /* [N] attempts spent on the step so far                          */
     Real *ctl, *cur; /* [nact][N] its held controls and smoothed actions               */
     Real *vnw;      /* [nm][N] fiber-velocity warm starts (the last call's roots)      */
-    int32_t *rkev;  /* [N] dynamics evaluations so far (RK kernels; bioim_eval_count) */
+    /* [N] RK kernels' counters: low 32 bits the dynamics evaluations so far
+     * (bioim_eval_count), high 32 the env steps finished (bioim_finished_count);
+     * one 64-bit update per launch */
+    uint64_t *rkev;
 };

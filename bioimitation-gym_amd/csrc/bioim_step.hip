@@ -3339,7 +3339,8 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         if constexpr (RK) {
             GAT(st.pend, env, (size_t)N) = suspend ? 1 : 0;
             /* evaluations: the attempts', plus one realize per finished step and per reset */
-            GAT(st.rkev, env, (size_t)N) += launch_evals + (suspend ? 0 : 1) + (do_reset && mode == 0 ? 1 : 0);
+            GAT(st.rkev, env, (size_t)N) += (uint64_t)(launch_evals + (suspend ? 0 : 1) + (do_reset && mode == 0 ? 1 : 0)) +
+                                            ((uint64_t)(mode == 0 && !suspend) << 32);
             if (a.traj && (mode == 0 || (osim && a.osim_op == BIOIM_OSIM_INTEGRATE))) GAT(a.traj_n, env, N) = traj_k;
             if (suspend) {
                 GAT(st.rkt, env, (size_t)N) = rk_t; GAT(st.rkh, env, (size_t)N) = rk_h; GAT(st.rka, env, (size_t)N) = rk_attempts;
@@ -4040,7 +4041,7 @@ template <typename Real> size_t state_layout(bioim_handle_t *h, char *base, DSta
     size_t opd = take(sizeof(int32_t) * n), ork = take(sizeof(double) * n), orh = take(sizeof(double) * n),
            ora = take(sizeof(int32_t) * n), octl = take(sizeof(Real) * na1 * n), ocur = take(sizeof(Real) * na1 * n),
            ovn = take(sizeof(Real) * nm1 * n);
-    size_t oev = take(sizeof(int32_t) * n);
+    size_t oev = take(sizeof(uint64_t) * n);
     if (st) {
         st->q = (Real *)(base + oq); st->u = (Real *)(base + ou); st->act = (Real *)(base + oa);
         st->lce = (Real *)(base + ol); st->hist = (Real *)(base + oh); st->last = (Real *)(base + olast);
@@ -4050,7 +4051,7 @@ template <typename Real> size_t state_layout(bioim_handle_t *h, char *base, DSta
         st->pend = (int32_t *)(base + opd); st->rkt = (double *)(base + ork); st->rkh = (double *)(base + orh);
         st->rka = (int32_t *)(base + ora); st->ctl = (Real *)(base + octl); st->cur = (Real *)(base + ocur);
         st->vnw = (Real *)(base + ovn);
-        st->rkev = (int32_t *)(base + oev);
+        st->rkev = (uint64_t *)(base + oev);
     }
     return off;
 }
@@ -4627,9 +4628,9 @@ int bioim_reset_count(bioim_handle_t *h, uint64_t *total) {
     return 0;
 }
 
-/* dynamics evaluations of the RK integrator so far, summed over the envs */
-int bioim_eval_count(bioim_handle_t *h, uint64_t *total) {
-    if (!h || !total) return fail(BIOIM_E_ARG, "bioim_eval_count: bad arguments");
+/* one of the per-env RK counters of the state (DState::rkev) summed over the envs */
+static int rk_counter(bioim_handle_t *h, uint64_t *total, bool fin, const char *who) {
+    if (!h || !total) return fail(BIOIM_E_ARG, std::string(who) + ": bad arguments");
     HIPCHK(hipSetDevice(h->device));
     std::vector<char> buf(h->state_bytes);
     HIPCHK(hipStreamSynchronize(h->stream));
@@ -4639,14 +4640,23 @@ int bioim_eval_count(bioim_handle_t *h, uint64_t *total) {
     if (h->precision == 64) {
         DState<double> hs;
         state_layout<double>(h, buf.data(), &hs);
-        for (int e = 0; e < h->n; ++e) sum += (uint32_t)hs.rkev[e];
+        for (int e = 0; e < h->n; ++e) sum += (uint32_t)(fin ? hs.rkev[e] >> 32 : hs.rkev[e]);
     } else {
         DState<float> hs;
         state_layout<float>(h, buf.data(), &hs);
-        for (int e = 0; e < h->n; ++e) sum += (uint32_t)hs.rkev[e];
+        for (int e = 0; e < h->n; ++e) sum += (uint32_t)(fin ? hs.rkev[e] >> 32 : hs.rkev[e]);
     }
     *total = sum;
     return 0;
+}
+
+/* dynamics evaluations of the RK integrator so far, summed over the envs */
+int bioim_eval_count(bioim_handle_t *h, uint64_t *total) { return rk_counter(h, total, false, "bioim_eval_count"); }
+
+/* env steps the RK integrator finished so far (bioim_step launches whose
+ * ready[env] was 1), summed over the envs */
+int bioim_finished_count(bioim_handle_t *h, uint64_t *total) {
+    return rk_counter(h, total, true, "bioim_finished_count");
 }
 
 int bioim_query(const bioim_handle_t *h, int32_t *out) {

@@ -236,6 +236,12 @@ int bioim_set_rk_budget(bioim_handle_t *h, int attempts, uint8_t *ready_out);
  * 0 for handles that never ran the adaptive integrator.  No reference
  * counterpart (bench.py's evaluations per env step). */
 int bioim_eval_count(bioim_handle_t *h, uint64_t *total);
+/* Env steps the adaptive integrator (kind 1) has finished so far, summed
+ * over the handle's envs: the count of bioim_step rows whose ready flag was
+ * 1 (bioim_set_rk_budget).  Synchronizes the handle's streams.  No reference
+ * counterpart (bench.py counts the reference-integrator rate with it instead
+ * of reading ready[] after every launch). */
+int bioim_finished_count(bioim_handle_t *h, uint64_t *total);
 /* envs suspended mid-step (synchronizes the handle's stream) */
 int bioim_pending_count(bioim_handle_t *h);
 /* Optional per-env step mask (device [n], NULL = every env steps): an env

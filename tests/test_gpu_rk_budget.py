@@ -36,6 +36,8 @@ def _run_budget(env_id, n, T, acts, rows, budget, precision=64):
     res_r = np.zeros((T, n))
     res_d = np.zeros((T, n), dtype=np.uint8)
     launches = suspended = 0
+    ready_total = 0
+    fin0 = env.finished_count()
     while k.min() < T and launches < 40 * T:
         a = np.stack([acts[min(k[i], T - 1)][i] for i in range(n)])
         o, r, d, _ = env.step(torch.as_tensor(a, device=env.device, dtype=env.dtype))
@@ -44,8 +46,11 @@ def _run_budget(env_id, n, T, acts, rows, budget, precision=64):
         for i in np.nonzero(ready & (k < T))[0]:
             res_o[k[i], i], res_r[k[i], i], res_d[k[i], i] = o[i], r[i], d[i]
         suspended += int((~ready).sum())
+        ready_total += int(ready.sum())
         k += ready
         launches += 1
+    # bioim_finished_count (bench.py's reference-integrator rate) counts exactly the ready rows
+    assert env.finished_count() - fin0 == ready_total, (env.finished_count() - fin0, ready_total)
     pending = env.pending_count()
     env.close()
     return res_o, res_r, res_d, launches, suspended, pending, k

@@ -4,7 +4,11 @@ the launch lasts as long as its slowest wave, so the gap between the mean
 and the maximum wave duration is time lost to imbalance (resets, Newton
 iteration counts, divergent branches).
 
-    python tools/wavetime.py [env_id] [--no-reset-table]   (GPU box; build first on the CPU: --build)
+    python tools/wavetime.py [env_id] [--no-reset-table] [--rk]   (GPU box; build first on the CPU: --build)
+
+--rk: the reference integrator in 6-attempt budgeted launches (bench.py's
+reference_integrator_rate), burned in by finished steps; the per-wave cycles
+are then split by how many of the wave's envs finished their step in the launch.
 """
 import ctypes as C
 import os
@@ -34,13 +38,29 @@ L = _lib.load()
 f = L.bioim_debug_wavetime
 f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 n = 4096
-env = VectorEnv(env_id, n, precision=64, seed=1000, auto_reset=True)
+rk = '--rk' in sys.argv
+env = VectorEnv(env_id, n, config={'integrator': 'rk-merson'} if rk else None, precision=64, seed=1000,
+                auto_reset=True)
 env.set_reset_table('--no-reset-table' not in sys.argv)
+if rk:
+    env.set_rk_budget(6)
 gen = np.random.Generator(np.random.PCG64(0))
 acts = torch.as_tensor(gen.uniform(0, 1, size=(64, n, env.action_dim)), device=env.device)
 env.reset()
-for k in range(150):
-    env.step(acts[k % 64])
+if rk:
+    fin = torch.zeros(n, dtype=torch.int32, device=env.device)
+    k0 = 0
+    while k0 < 50 * 155 and (k0 % 10 or int(fin.sum()) < n * 155):
+        env.step(acts[k0 % 64])
+        fin += env.ready
+        k0 += 1
+else:
+    for k in range(150):
+        env.step(acts[k % 64])
+epw = 64 // env.lanes_per_env if env.lanes_per_env <= 64 else 1
+by_fin = {}
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+kms = []
 nw = env.launch['workgroups'] * env.launch['threads_per_workgroup'] // 64
 buf = (C.c_ulonglong * nw)()
 fvf = getattr(L, 'bioim_debug_fviter', None)
@@ -53,10 +73,20 @@ rows = []
 raw = []
 for k in range(20):
     r0 = int(env.done.sum()) if k else 0
+    torch.cuda.synchronize()
+    ev0.record()
     env.step(acts[k % 64])
+    ev1.record()
+    torch.cuda.synchronize()
+    kms.append(ev0.elapsed_time(ev1))
     f(buf, nw)
     d = np.array(buf[:], dtype=np.float64)
     raw.append([d])
+    if rk:
+        rd = env.ready.cpu().numpy().astype(np.int64)
+        nf = rd[:nw * epw].reshape(nw, epw).sum(1)
+        for c in range(epw + 1):
+            by_fin.setdefault(c, []).extend(d[nf == c].tolist())
     if fvf is not None:
         fvf(fvb, nt)
         it = np.array(fvb[:nt], dtype=np.float64).reshape(nw, 64)
@@ -76,6 +106,14 @@ if fv_rows:
 out = os.environ.get('WAVETIME_OUT')
 if out:   # raw per-wave cycles of the 20 launches, for offline analysis
     np.save(out, np.array([r[0] for r in raw]))
-print(f'{env_id} reset_table={"--no-reset-table" not in sys.argv}: {nw} waves, 20 launches; wave cycles '
+if rk:
+    for c in sorted(by_fin):
+        v = np.array(by_fin[c])
+        if len(v):
+            print(f'  waves with {c} of {epw} envs finishing their step: {len(v) / 20:.0f} per launch, cycles mean '
+                  f'{v.mean():.0f} max {v.max():.0f}')
+print(f'  launch (events) {np.mean(kms) * 1e3:.1f} us; max wave {a[:, 4].mean():.0f} memtime ticks '
+      f'(= {a[:, 4].mean() / (np.mean(kms) * 1e3):.0f} ticks per us of launch)')
+print(f'{env_id} rk={rk} reset_table={"--no-reset-table" not in sys.argv}: {nw} waves, 20 launches; wave cycles '
       f'mean {a[:, 0].mean():.0f}  p50 {a[:, 1].mean():.0f}  p90 {a[:, 2].mean():.0f}  p99 {a[:, 3].mean():.0f}  '
       f'max {a[:, 4].mean():.0f}; mean/max {np.mean(a[:, 0] / a[:, 4]):.3f}; dones per launch {a[:, 5].mean():.1f}')
