@@ -271,13 +271,13 @@ def main():
     acts = torch.as_tensor(gen.uniform(0.0, 1.0, size=(pool, n, A)), dtype=env.dtype, device=dev)
     env.reset()
     stream = torch.cuda.current_stream(dev)
-    k0 = a.burn_in + a.warmup
+    k0 = a.burn_in
     if a.rk_budget:
         # budgeted launches finish fewer than n steps each: burn in by finished env steps, so the
         # timed region sees envs as far past their resets (and as often fallen) as the unbudgeted run
         fin = torch.zeros(n, dtype=torch.int32, device=dev)
         k0 = 0
-        while k0 < 50 * (a.burn_in + a.warmup) and (k0 % 10 or int(fin.sum()) < n * (a.burn_in + a.warmup)):
+        while k0 < 50 * a.burn_in and (k0 % 10 or int(fin.sum()) < n * a.burn_in):
             env.step(acts[k0 % pool])
             fin += env.ready
             k0 += 1
@@ -285,16 +285,27 @@ def main():
         for k in range(k0):
             env.step(acts[k % pool])
     torch.cuda.synchronize(dev)
+    # the counters first, then the W warm-up steps: a counter read copies the state to the host and
+    # leaves the GPU idle for milliseconds, and launches after an idle GPU run slower until its clocks
+    # are back -- the untimed warm-up, not the timed steps, absorbs that.  done_rate and
+    # evals_per_env_step therefore cover warm-up + timed steps; value covers the timed steps only
     resets0 = sum(h.reset_count() for h in handles)
     rk = a.integrator == 'rk-merson'
     rk = rk and all(hasattr(h._L, 'bioim_eval_count') for h in handles)   # older A/B builds lack the counter
     evals0 = sum(h.eval_count() for h in handles) if rk else 0
+    # budgeted RK: envs whose step finished, from the launches' own counter (bioim_finished_count),
+    # minus the warm-up's (summed from ready[] on the device during the warm-up)
+    fin0 = env.finished_count() if a.rk_budget else 0
+    wfin = torch.zeros(n, dtype=torch.int32, device=dev) if a.rk_budget else None
+    for k in range(a.warmup):
+        env.step(acts[(k0 + k) % pool])
+        if wfin is not None:
+            wfin += env.ready
+    k0 += a.warmup
 
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         dist.barrier()
-    # budgeted RK: envs whose step finished, from the launches' own counter (bioim_finished_count)
-    fin0 = env.finished_count() if a.rk_budget else 0
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record(stream)
@@ -311,7 +322,9 @@ def main():
         tt = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt[0])
-    steps_local = env.finished_count() - fin0 if a.rk_budget else n * a.steps
+    fin1 = env.finished_count() if a.rk_budget else 0
+    steps_local = fin1 - fin0 - int(wfin.sum()) if a.rk_budget else n * a.steps
+    steps_counted = fin1 - fin0 if a.rk_budget else n * (a.warmup + a.steps)   # the counters' interval
     if dist:
         st_ = torch.tensor([steps_local], dtype=torch.float64)
         dist.all_reduce(st_)
@@ -319,7 +332,7 @@ def main():
     else:
         steps_total = steps_local
     value = steps_total / t_max
-    done_rate = (sum(h.reset_count() for h in handles) - resets0) / max(steps_local, 1)
+    done_rate = (sum(h.reset_count() for h in handles) - resets0) / max(steps_counted, 1)
     if rank == 0:
         real_bytes = 8 if a.precision == 64 else 4
         if a.mixed:   # env-weighted mean over the segments
@@ -363,7 +376,7 @@ def main():
         if a.rk_budget:
             line['finished_env_steps'] = steps_total
         if rk:
-            line['evals_per_env_step'] = (sum(h.eval_count() for h in handles) - evals0) / max(steps_local, 1)
+            line['evals_per_env_step'] = (sum(h.eval_count() for h in handles) - evals0) / max(steps_counted, 1)
         if not a.no_cpu_baseline and world == 1:
             line['cpu_baseline'] = cpu_baseline(a.env_id)
         if world == 1 and not a.mixed and not a.no_single_env:
@@ -380,6 +393,7 @@ def main():
 
 
 RK_BUDGET = 6   # attempts per env per launch (DESIGN.md §3 sweep: best at 4096 envs for every ID measured)
+RK_WARMUP = 10  # untimed launches between the counter reads and the timed launches (at least --warmup)
 
 
 def reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist):
@@ -418,17 +432,27 @@ def reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist):
         for f, e in zip(fins, segs):
             f += e.ready
     k0 = 0
-    while k0 < 50 * (a.burn_in + a.warmup) and (k0 % 10 or int(fin.sum()) < n * (a.burn_in + a.warmup)):
+    while k0 < 50 * a.burn_in and (k0 % 10 or int(fin.sum()) < n * a.burn_in):
         env.step(acts[k0 % pool])
         count_ready()
         k0 += 1
+    # the counters, then the warm-up launches (as in main(): a counter read idles the GPU, and the
+    # launches after it run slower until the clocks are back)
     resets0 = sum(e.reset_count() for e in segs)
     counted = hasattr(segs[0]._L, 'bioim_eval_count')    # older A/B builds lack the counter
     evals0 = sum(e.eval_count() for e in segs) if counted else 0
     # finished steps from the launches' own per-env counter (bioim_finished_count), so the timed
-    # region holds the step launches only (summing ready[] after each launch cost 1 % on C3)
+    # region holds the step launches only (summing ready[] after each launch cost 1 % on C3); the
+    # warm-up's finished steps are summed from ready[] on the device and subtracted
     in_kernel = hasattr(segs[0]._L, 'bioim_finished_count')
     fin0 = sum(e.finished_count() for e in segs) if in_kernel else 0
+    fin.zero_()
+    warm = max(a.warmup, RK_WARMUP)
+    for k in range(warm):
+        env.step(acts[k0 % pool])
+        count_ready()
+        k0 += 1
+    warm_fin = fin.clone()
     fin.zero_()
     if dist:
         dist.barrier()
@@ -442,7 +466,11 @@ def reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist):
     wall = time.perf_counter() - t0
     if dist:
         dist.barrier()
-    local = sum(e.finished_count() for e in segs) - fin0 if in_kernel else int(fin.sum())
+    fin1 = sum(e.finished_count() for e in segs) if in_kernel else 0
+    local = fin1 - fin0 - int(warm_fin.sum()) if in_kernel else int(fin.sum())
+    # the counters' interval (warm-up + timed launches) for the per-step statistics
+    counted_steps = fin1 - fin0 if in_kernel else local + int(warm_fin.sum())
+    counted_launches = warm + a.steps
     tot, t_max = float(local), wall
     if dist:
         tt = torch.tensor([wall], dtype=torch.float64)
@@ -453,13 +481,13 @@ def reference_integrator_rate(a, acts, pool, dev, stream, rank, world, dist):
         tot = float(st_[0])
     rate = {'value': tot / t_max, 'unit': 'finished env-steps/s', 'integrator': 'rk-merson', 'accuracy': 1e-3,
             'rk_budget': RK_BUDGET, 'launches': a.steps, 'ms_per_launch': t_max / a.steps * 1e3,
-            'finished_env_steps': tot, 'done_rate': (sum(e.reset_count() for e in segs) - resets0) / max(local, 1),
-            'evals_per_env_step': (sum(e.eval_count() for e in segs) - evals0) / max(local, 1) if counted else None,
+            'finished_env_steps': tot, 'done_rate': (sum(e.reset_count() for e in segs) - resets0) / max(counted_steps, 1),
+            'evals_per_env_step': (sum(e.eval_count() for e in segs) - evals0) / max(counted_steps, 1) if counted else None,
             # share of the launches' attempt capacity (RK_BUDGET attempts x 5 evaluations per env) that
             # envs spent idle after finishing their step (attempt evaluations = all evaluations minus one
             # realize per finished step and one per reset)
-            'launch_idle_share': (1.0 - (sum(e.eval_count() for e in segs) - evals0 - local -
-                                         (sum(e.reset_count() for e in segs) - resets0)) / (a.steps * n * 5 * RK_BUDGET))
+            'launch_idle_share': (1.0 - (sum(e.eval_count() for e in segs) - evals0 - counted_steps -
+                                         (sum(e.reset_count() for e in segs) - resets0)) / (counted_launches * n * 5 * RK_BUDGET))
             if counted else None,
             'note': "the reference's integrator (opensim_wrapper.py:287-301) on the same workload; "
                     'GPU parity vs the oracle in tests/test_gpu_parity.py (RK) and tests/test_gpu_rk_budget.py'}

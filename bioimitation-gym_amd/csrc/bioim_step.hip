@@ -3019,6 +3019,11 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
          * muscle_walking_imitation_env2D.py:158-225).  The realize call left
          * the coordinates (QF/UF), frames (KB), contact wrenches (CW) and limit
          * forces (LIM) in LDS; report points first. */
+#ifdef BIOIM_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long rp_t0 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         using OL = ObsLayout<T>;
         const Real x0 = D.x0;
         Real *ob = lds + LY::OBS;
@@ -3148,6 +3153,12 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         wave_sync();
         if (reported_reset || osim) break;
 
+#ifdef BIOIM_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long rp_t1 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         /* ---- reward (get_reward) and termination (is_done); group sums are
          * xor butterflies, so every lane holds bitwise-identical totals */
         {
@@ -3246,6 +3257,15 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             GAT(a.info, (size_t)env * a.info_stride + lane, (size_t)N * a.info_stride) = iv;
         }
         wave_sync();
+#ifdef BIOIM_STAMPS
+        {   /* the report of the first env of workgroup 0: observation part, reward + done part, reports */
+            __builtin_amdgcn_sched_barrier(0);
+            const unsigned long long rp_t2 = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            if (blockIdx.x == 0 && threadIdx.x == 0) { g_stamps[19] += rp_t1 - rp_t0; g_stamps[20] += rp_t2 - rp_t1; g_stamps[21] += 1; }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#endif
         if (done && a.auto_reset) {
             pending_reset = true;
             do_reset = true;

@@ -7,15 +7,19 @@ sys.path[:0] = [os.path.join(REPO, 'bioimitation-gym_amd')]
 import numpy as np, torch
 from bioimitation import _lib
 from bioimitation.vector_env import VectorEnv
-prec = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-env_id = sys.argv[2] if len(sys.argv) > 2 else 'MuscleWalkingImitation2D-v0'
+args = [x for x in sys.argv[1:] if not x.startswith('--')]
+prec = int(args[0]) if args else 64
+env_id = args[1] if len(args) > 1 else 'MuscleWalkingImitation2D-v0'
 L = _lib.load()
 f = L.bioim_debug_stamps
 f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-env = VectorEnv(env_id, 4096, precision=prec, seed=1, auto_reset=True)
+rk = '--rk' in sys.argv
+env = VectorEnv(env_id, 4096, config={'integrator': 'rk-merson'} if rk else None, precision=prec, seed=1,
+                auto_reset=True)
+if rk:
+    env.set_rk_budget(6)
 env.reset()
 buf = (C.c_ulonglong * 24)()
-steps = 30
 steps = 30
 acts = torch.rand((steps + 5, 4096, env.action_dim), device=env.device, dtype=env.dtype)
 for k in range(5):
@@ -36,6 +40,9 @@ for i, n in enumerate(names):
     print(f'  {n:32s} {buf[i] / calls:9.0f} cyc  {100.0 * buf[i] / tot:5.1f} %')
 print(f'  per launch: loop {buf[10] / steps:.0f} cyc, of which dynamics {tot / steps:.0f}; '
       f'model-image staging {buf[11] / steps:.0f} cyc')
+if buf[21]:
+    print(f'  report (wg 0, env 0): {buf[21]} reports, per report: observation {buf[19] / buf[21]:.0f} cyc, '
+          f'reward + done + writes {buf[20] / buf[21]:.0f} cyc')
 if buf[13]:
     print(f'  solve_fv (wg 0, env 0 lanes): mean iterations {buf[12] / buf[13]:.2f} over {buf[13]} solves, '
           f'{buf[14]} hit it_max')
