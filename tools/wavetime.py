@@ -82,11 +82,12 @@ for k in range(20):
     f(buf, nw)
     d = np.array(buf[:], dtype=np.float64)
     raw.append([d])
-    if rk:
-        rd = env.ready.cpu().numpy().astype(np.int64)
-        nf = rd[:nw * epw].reshape(nw, epw).sum(1)
-        for c in range(epw + 1):
-            by_fin.setdefault(c, []).extend(d[nf == c].tolist())
+    # RK: envs of the wave that finished their step in the launch; semi-implicit: envs that were done
+    # (and reset in the launch)
+    rd = (env.ready if rk else env.done).cpu().numpy().astype(np.int64)
+    nf = rd[:nw * epw].reshape(nw, epw).sum(1)
+    for c in range(epw + 1):
+        by_fin.setdefault(c, []).extend(d[nf == c].tolist())
     if fvf is not None:
         fvf(fvb, nt)
         it = np.array(fvb[:nt], dtype=np.float64).reshape(nw, 64)
@@ -106,12 +107,15 @@ if fv_rows:
 out = os.environ.get('WAVETIME_OUT')
 if out:   # raw per-wave cycles of the 20 launches, for offline analysis
     np.save(out, np.array([r[0] for r in raw]))
-if rk:
-    for c in sorted(by_fin):
-        v = np.array(by_fin[c])
-        if len(v):
-            print(f'  waves with {c} of {epw} envs finishing their step: {len(v) / 20:.0f} per launch, cycles mean '
-                  f'{v.mean():.0f} max {v.max():.0f}')
+for c in sorted(by_fin):
+    v = np.array(by_fin[c])
+    if len(v):
+        what = 'finishing their step' if rk else 'done (reset in the launch)'
+        print(f'  waves with {c} of {epw} envs {what}: {len(v) / 20:.1f} per launch, cycles mean '
+              f'{v.mean():.0f} p99 {np.percentile(v, 99):.0f} max {v.max():.0f}')
+allw = np.concatenate([r[0] for r in raw])
+top = allw >= np.percentile(allw, 99.5)
+print(f'  slowest 0.5 % of waves: {top.sum()} waves')
 print(f'  launch (events) {np.mean(kms) * 1e3:.1f} us; max wave {a[:, 4].mean():.0f} memtime ticks '
       f'(= {a[:, 4].mean() / (np.mean(kms) * 1e3):.0f} ticks per us of launch)')
 print(f'{env_id} rk={rk} reset_table={"--no-reset-table" not in sys.argv}: {nw} waves, 20 launches; wave cycles '
