@@ -329,7 +329,12 @@ def rllib_env_offset(config, num_envs):
     v = int(getattr(config, 'vector_index', 0) or 0)
     if v * num_envs >= (1 << RLLIB_WORKER_SHIFT):
         raise ValueError(f'rllib_creator: vector_index {v} x num_envs {num_envs} exceeds 2**{RLLIB_WORKER_SHIFT} envs per worker')
-    return (w << RLLIB_WORKER_SHIFT) + v * num_envs
+    off = (w << RLLIB_WORKER_SHIFT) + v * num_envs
+    # bioim_set_env_offset takes a C int and the kernel forms env_offset + env in 32 bits
+    if w < 0 or v < 0 or off + num_envs > (1 << 31) - 1:
+        raise ValueError(f'rllib_creator: worker_index {w} / vector_index {v} put the global env index '
+                         f'{off} + {num_envs} past 2**31 - 1 (at most {(1 << (31 - RLLIB_WORKER_SHIFT)) - 1} workers)')
+    return off
 
 
 def register_with_gym():

@@ -437,7 +437,7 @@ class OsimModelFacade:
             warnings.warn(f'state storage: {k} accepted integration steps in one env step, the buffer held '
                           f'{cap}; the rows after the first {cap} are not recorded (buffer grown to '
                           f'{max(2 * cap, k)} rows for the next steps)', RuntimeWarning)
-            env.enable_state_storage(max(2 * cap, k))
+            env.grow_state_storage(max(2 * cap, k))   # applied before the next step's launch
         return rows
 
     def _realizer(self, k):

@@ -176,6 +176,20 @@ class VectorEnv:
             self.storage_rows = self.storage_count = None
         _lib.check(self._L.bioim_set_state_storage(self._h, self._ptr(self.storage_rows), int(capacity),
                                                    self._ptr(self.storage_count)))
+        self._storage_grow = 0
+
+    def grow_state_storage(self, capacity: int):
+        """Ask for at least ``capacity`` storage rows from the NEXT ``step()``
+        on: the reallocation (which zeroes ``storage_rows`` / ``storage_count``
+        for every env of the batch) is deferred to just before that step's
+        launch, so every reader of the current step's rows still sees them."""
+        self._storage_grow = max(getattr(self, '_storage_grow', 0), int(capacity))
+
+    def _apply_storage_growth(self):
+        k = getattr(self, '_storage_grow', 0)
+        if k and getattr(self, 'storage_rows', None) is not None and k > self.storage_rows.shape[1]:
+            self.enable_state_storage(k)
+        self._storage_grow = 0
 
     def set_rk_budget(self, attempts: int):
         """Budgeted steps for the 'rk-merson' integrator (``bioim_set_rk_budget``):
@@ -222,6 +236,8 @@ class VectorEnv:
         if controls is not None:
             ctl = torch.as_tensor(controls, dtype=self.dtype, device=self.device).reshape(ids.numel(), self.action_dim)
             ctl = ctl.contiguous()
+        if getattr(self, '_storage_grow', 0):
+            self._apply_storage_growth()
         self._bind_stream()
         _lib.check(self._L.bioim_osim(self._h, OSIM_OPS[op], self._ptr(ids), ids.numel(), self._ptr(ctl),
                                       self._ptr(self.obs) if want_obs else None, self._ptr(self.osim_report)))
@@ -283,6 +299,8 @@ class VectorEnv:
         if a.dtype != self.dtype or a.device != self.device or not a.is_contiguous():
             a = a.to(device=self.device, dtype=self.dtype).contiguous()
         assert a.shape == (self.num_envs, self.action_dim), a.shape
+        if getattr(self, '_storage_grow', 0):
+            self._apply_storage_growth()
         self._bind_stream()
         _lib.check(self._L.bioim_step(self._h, self._ptr(a), self._ptr(self.obs), self._ptr(self.reward),
                                       self._ptr(self.done), self._ptr(self.info)))
@@ -317,6 +335,11 @@ class VectorEnv:
         n = C.c_uint64()
         _lib.check(self._L.bioim_finished_count(self._h, C.byref(n)))
         return int(n.value)
+
+    def set_rk_counters(self, evals: int = 0, finished: int = 0):
+        """Set every env's evaluation / finished-step counters
+        (bioim_set_rk_counters; 32 bits each per env, wrapping independently)."""
+        _lib.check(self._L.bioim_set_rk_counters(self._h, int(evals) & 0xffffffff, int(finished) & 0xffffffff))
 
     def sync(self):
         _lib.check(self._L.bioim_sync(self._h))

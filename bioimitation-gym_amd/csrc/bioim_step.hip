@@ -3291,6 +3291,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                     has_last = 0;
                     rk_hnext = 0;   /* reset_manager: a new integrator (opensim_wrapper.py:287-291) */
                     resets += 1;
+                    if constexpr (RK) launch_evals -= 1;   /* no reset realize ran: not an evaluation */
                     if constexpr (NM > 0) {
 #pragma unroll
                         for (int j = 0; j < MPL; ++j) {
@@ -3358,9 +3359,14 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
         if (RK || mode == 1 || (osim && a.osim_op == BIOIM_OSIM_EQUILIBRATE)) GAT(st.hrk, env, (size_t)N) = rk_hnext;
         if constexpr (RK) {
             GAT(st.pend, env, (size_t)N) = suspend ? 1 : 0;
-            /* evaluations: the attempts', plus one realize per finished step and per reset */
-            GAT(st.rkev, env, (size_t)N) += (uint64_t)(launch_evals + (suspend ? 0 : 1) + (do_reset && mode == 0 ? 1 : 0)) +
-                                            ((uint64_t)(mode == 0 && !suspend) << 32);
+            /* evaluations (low 32 bits): the attempts', plus one realize per
+             * finished step and per reset that ran one (a reset-table reset
+             * took one back, see above); finished steps (high 32 bits).  Two
+             * independent wrapping halves: no carry from one into the other */
+            const uint64_t ev0 = GAT(st.rkev, env, (size_t)N);
+            const uint32_t ev_lo = (uint32_t)ev0 + (uint32_t)(launch_evals + (suspend ? 0 : 1) + (do_reset && mode == 0 ? 1 : 0));
+            const uint32_t ev_hi = (uint32_t)(ev0 >> 32) + (uint32_t)(mode == 0 && !suspend);
+            GAT(st.rkev, env, (size_t)N) = ((uint64_t)ev_hi << 32) | ev_lo;
             if (a.traj && (mode == 0 || (osim && a.osim_op == BIOIM_OSIM_INTEGRATE))) GAT(a.traj_n, env, N) = traj_k;
             if (suspend) {
                 GAT(st.rkt, env, (size_t)N) = rk_t; GAT(st.rkh, env, (size_t)N) = rk_h; GAT(st.rka, env, (size_t)N) = rk_attempts;
@@ -4677,6 +4683,27 @@ int bioim_eval_count(bioim_handle_t *h, uint64_t *total) { return rk_counter(h, 
  * ready[env] was 1), summed over the envs */
 int bioim_finished_count(bioim_handle_t *h, uint64_t *total) {
     return rk_counter(h, total, true, "bioim_finished_count");
+}
+
+int bioim_set_rk_counters(bioim_handle_t *h, uint32_t evals, uint32_t finished) {
+    if (!h) return fail(BIOIM_E_ARG, "bioim_set_rk_counters: null handle");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipStreamSynchronize(h->side));
+    std::vector<char> buf(h->state_bytes);
+    HIPCHK(hipMemcpy(buf.data(), h->state_buf, h->state_bytes, hipMemcpyDeviceToHost));
+    const uint64_t v = ((uint64_t)finished << 32) | evals;
+    if (h->precision == 64) {
+        DState<double> hs;
+        state_layout<double>(h, buf.data(), &hs);
+        for (int e = 0; e < h->n; ++e) hs.rkev[e] = v;
+    } else {
+        DState<float> hs;
+        state_layout<float>(h, buf.data(), &hs);
+        for (int e = 0; e < h->n; ++e) hs.rkev[e] = v;
+    }
+    HIPCHK(hipMemcpy(h->state_buf, buf.data(), h->state_bytes, hipMemcpyHostToDevice));
+    return 0;
 }
 
 int bioim_query(const bioim_handle_t *h, int32_t *out) {

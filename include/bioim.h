@@ -242,6 +242,13 @@ int bioim_eval_count(bioim_handle_t *h, uint64_t *total);
  * counterpart (bench.py counts the reference-integrator rate with it instead
  * of reading ready[] after every launch). */
 int bioim_finished_count(bioim_handle_t *h, uint64_t *total);
+/* Sets every env's two RK counters (the evaluations and the finished steps
+ * that bioim_eval_count / bioim_finished_count sum) to the given values,
+ * e.g. to restart the counting of a measurement window or to carry counts
+ * across a handle re-creation.  Each counter is 32 bits per env and wraps on
+ * its own (no carry into the other).  Synchronizes the handle's streams.  No
+ * reference counterpart. */
+int bioim_set_rk_counters(bioim_handle_t *h, uint32_t evals, uint32_t finished);
 /* envs suspended mid-step (synchronizes the handle's stream) */
 int bioim_pending_count(bioim_handle_t *h);
 /* Optional per-env step mask (device [n], NULL = every env steps): an env

@@ -217,6 +217,16 @@ def test_rllib_creator_dispatches_on_num_envs(monkeypatch):
     assert calls[3] == ('vec', env_id, 256, {'horizon': 3}, 0, 64, (3 << envs.RLLIB_WORKER_SHIFT) + 256)
     with pytest.raises(ValueError):
         envs.rllib_env_offset(EnvContextV(), 1 << envs.RLLIB_WORKER_SHIFT)
+
+    # the global index must fit the C int env_offset
+    class EnvContextBig(EnvContext):
+        worker_index = 1 << (31 - envs.RLLIB_WORKER_SHIFT)
+    last = (1 << (31 - envs.RLLIB_WORKER_SHIFT)) - 1
+    class EnvContextLast(EnvContext):
+        worker_index = last
+    with pytest.raises(ValueError):
+        envs.rllib_env_offset(EnvContextBig(), 16)
+    assert envs.rllib_env_offset(EnvContextLast(), 16) == last << envs.RLLIB_WORKER_SHIFT
     with pytest.raises(NotImplementedError):
         envs.rllib_creator('MuscleJumpingImitation2D-v0')
 

@@ -455,6 +455,11 @@ def test_state_storage_overflow_grows_buffer(tmp_path):
         env.step(a)
     om = env.osim_model
     lost = om.storage_truncated_rows
+    # the growth is deferred to the next launch, so the overflowing
+    # step's rows and count stay readable until then
+    assert env._env.storage_rows.shape[1] == 2 and int(env._env.storage_count[0]) > 2
+    assert env._env._storage_grow >= 4
+    env._env._apply_storage_growth()
     assert lost > 0 and env._env.storage_rows.shape[1] >= 4
     assert env._env.storage_rows.shape[1] >= int(env._env.storage_count[0])
     clean = False

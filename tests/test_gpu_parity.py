@@ -900,7 +900,12 @@ def test_parity_200_steps_muscle_tracking_drive(env_id):
                                                ('MuscleLockedKneeImitation3D-v0', 'semi-implicit'),
                                                ('MuscleWalkingImitation2D-v0', 'rk-merson'),
                                                ('TorqueWalkingImitation2D-v0', 'semi-implicit'),
-                                               ('TorqueWalkingImitation3D-v0', 'semi-implicit')])
+                                               ('TorqueWalkingImitation3D-v0', 'semi-implicit'),
+                                               # the Muscle3D topology (C4 Running3D, C5 Palsy3D
+                                               # with its raw action) and the torque branch of the planar RK kernel
+                                               ('MuscleRunningImitation3D-v0', 'semi-implicit'),
+                                               ('MusclePalsyImitation3D-v0', 'semi-implicit'),
+                                               ('TorqueWalkingImitation2D-v0', 'rk-merson')])
 def test_reset_table_matches_reset_realize(env_id, integrator):
     """In-kernel auto-resets from the reset table (bioim_set_reset_table, the
     default) against the reset realize run in the step launch (table off):
@@ -942,9 +947,121 @@ def test_reset_table_matches_reset_realize(env_id, integrator):
             np.testing.assert_array_equal(a.get_state(), b.get_state())
     assert a.reset_table_rows == a.pack.nrows and b.reset_table_rows == 0
     assert resets > 20, resets
+    if integrator == 'rk-merson':
+        # a table reset runs no realize, so it adds no evaluation;
+        # the realize path counts one per reset
+        assert b.eval_count() - a.eval_count() == resets, (b.eval_count(), a.eval_count(), resets)
+        assert a.finished_count() == b.finished_count() == n * T
     # observed 4.1e-12 (q'' of reset rows: the fiber-velocity root's last bits; torque models: M^-1 tau
     # from the inverse-dynamics kernel's M against the realize's factorization)
     assert worst < 1e-10, worst
     print(f'{env_id} {integrator}: {resets} auto-resets over {T} steps x {n} envs; table vs realize obs max rel diff {worst:.1e}')
     a.close()
     b.close()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+def test_c5_fused_bench_size_reset_table_vs_realize():
+    """config C5 as the bench runs it — 2048
+    LockedKnee3D + 2048 Palsy3D envs in ONE fused launch with in-kernel
+    auto-reset — with the reset table (default) against the reset realize in
+    the launch (table off on both segments): 160 steps from reference-rule
+    rows, every reward / done / info and (every 8 steps) the whole state
+    bit-equal, obs within 1e-10, the resets counted."""
+    import torch
+    from bioimitation import _lib
+    from bioimitation.vector_env import MixedVectorEnv
+    segs = [('MuscleLockedKneeImitation3D-v0', 2048), ('MusclePalsyImitation3D-v0', 2048)]
+    _lib.load().bioim_set_group_fusion(1)
+    a = MixedVectorEnv(segs, precision=64, seed=5, auto_reset=True)
+    b = MixedVectorEnv(segs, precision=64, seed=5, auto_reset=True)
+    for e in b.envs:
+        e.set_reset_table(False)
+    rng = np.random.default_rng(8)
+    for ea, eb in zip(a.envs, b.envs):
+        rows = rng.integers(0, ea.pack.reset_hi + 1, size=ea.num_envs)
+        ea.reset(ref_index=rows)
+        eb.reset(ref_index=rows)
+    g = torch.Generator(device='cuda').manual_seed(9)
+    same = lambda x, y: bool(((x == y) | (x.isnan() & y.isnan())).all()) if x.is_floating_point() else torch.equal(x, y)
+    T, resets, worst = 160, 0, 0.0
+    for t in range(T):
+        act = torch.rand((a.num_envs, a.action_dim), generator=g, device=a.device, dtype=torch.float64)
+        oa, ra, da, ia = (x.clone() for x in a.step(act))
+        assert a.last_step_fused, 'the C5 pair must run as one fused launch (table on)'
+        ob, rb, db, ib = b.step(act)
+        assert b.last_step_fused, 'the C5 pair must run as one fused launch (table off)'
+        assert same(da, db) and same(ra, rb) and same(ia, ib), t
+        resets += int(da.sum())
+        worst = max(worst, float(torch.nan_to_num((oa - ob).abs().div(ob.abs().clamp(min=1.0)), nan=0.0).max()))
+        if t % 8 == 7 or t == T - 1:
+            for ea, eb in zip(a.envs, b.envs):
+                np.testing.assert_array_equal(ea.get_state(), eb.get_state())
+    for ea, eb in zip(a.envs, b.envs):
+        assert ea.reset_table_rows == ea.pack.nrows and eb.reset_table_rows == 0
+    assert resets > 200, resets
+    assert worst < 1e-10, worst
+    print(f'C5 fused 2048 + 2048: {resets} auto-resets over {T} steps; table vs realize obs max rel diff {worst:.1e}')
+    a.close()
+    b.close()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+def test_c4_auto_reset_rows_vs_oracle_reset():
+    """config C4's per-GPU batch (4096 Running3D envs,
+    256 workgroups) with the bench's U[0,1] excitations and in-kernel
+    auto-reset from the reset table.  For every env of a strided sample that
+    terminates, the post-reset row the kernel drew is read back from the
+    state (its time is the reference row's time) and the post-reset
+    observation and state are checked against the oracle's own reset of that
+    row (Env.reset, opensim_wrapper.py:287-297): t, istep, q, u, activations
+    and has_last / done equal, fiber lengths and obs within 1e-9."""
+    import torch
+    import oracle
+    from bioimitation.vector_env import VectorEnv
+    env_id, n, T = 'MuscleRunningImitation3D-v0', 4096, 160
+    env = VectorEnv(env_id, n, precision=64, seed=13, auto_reset=True)
+    pk = env.pack
+    rows0 = np.random.default_rng(14).integers(0, pk.reset_hi + 1, size=n)
+    env.reset(ref_index=rows0)
+    times = np.asarray(pk.ref_time[:pk.nrows])
+    nd, nm = pk.ndof, pk.nmuscle
+    orc = oracle.Oracle(pk)
+    bufs = orc.new_envs(1)
+    sample = np.zeros(n, bool)
+    sample[::5] = True
+    sample[-16:] = True                   # the last workgroup
+    g = torch.Generator(device='cuda').manual_seed(15)
+    checked, resets, worst_obs, worst_lce, drawn = 0, 0, 0.0, 0.0, set()
+    for t in range(T):
+        act = torch.rand((n, env.action_dim), generator=g, device=env.device, dtype=torch.float64)
+        obs, rew, done, _ = env.step(act)
+        d = done.cpu().numpy().astype(bool)
+        resets += int(d.sum())
+        idx = np.nonzero(d & sample)[0]
+        if len(idx) == 0:
+            continue
+        st = env.get_state()
+        ob = obs.cpu().numpy()
+        for i in idx:
+            r = np.nonzero(times == st[i, 0])[0]
+            assert len(r) == 1, (t, i, st[i, 0])
+            r = int(r[0])
+            assert 0 <= r <= pk.reset_hi, r
+            drawn.add(r)
+            o_ref = orc.reset(bufs, 0, r)
+            s_ref = orc.get_state(bufs, 0)
+            # t, istep, has_last, (old_px is per-episode history), done
+            assert st[i, 0] == s_ref[0] and st[i, 1] == s_ref[1] and st[i, 2] == 0 and st[i, 4] == 0, (i, r)
+            q0 = 5
+            np.testing.assert_array_equal(st[i, q0:q0 + 2 * nd + nm], s_ref[q0:q0 + 2 * nd + nm])  # q, u, activations
+            lce, lref = st[i, q0 + 2 * nd + nm:q0 + 2 * nd + 2 * nm], s_ref[q0 + 2 * nd + nm:q0 + 2 * nd + 2 * nm]
+            worst_lce = max(worst_lce, float(np.max(np.abs(lce - lref) / np.abs(lref))))
+            worst_obs = max(worst_obs, float(_rel(ob[i], o_ref).max()))
+            checked += 1
+    assert env.reset_table_rows == pk.nrows
+    print(f'C4 4096 envs: {resets} auto-resets over {T} steps, {checked} sampled post-reset rows '
+          f'({len(drawn)} distinct reference rows) vs the oracle reset: obs {worst_obs:.1e}, fiber lengths {worst_lce:.1e}')
+    assert checked >= 100 and len(drawn) >= 30, (checked, len(drawn))
+    assert worst_obs < 1e-9 and worst_lce < 1e-9, (worst_obs, worst_lce)
+    env.close()

@@ -205,3 +205,28 @@ def test_mixed_batch_rk_budget_matches_segments_alone():
     assert sum(e.reset_count() for e in mixed.envs) == sum(e.reset_count() for e in alone)
     for e in alone + [mixed]:
         e.close()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs a HIP GPU')
+def test_rk_counters_wrap_independently():
+    """each env's RK evaluation count (low 32 bits of its counter)
+    and finished-step count (high 32 bits) wrap on their own.  Seeded just
+    below 2**32, the evaluation half wraps after a few steps while the
+    finished half counts exactly the finished steps (no carry into it)."""
+    import torch
+    from bioimitation.vector_env import VectorEnv
+    n, T = 64, 3
+    runs = []
+    for seed_ev in (0, 2**32 - 50):
+        env = VectorEnv('MuscleWalkingImitation2D-v0', n, config={'integrator': 'rk-merson'}, precision=64, seed=2)
+        env.reset(ref_index=np.arange(n) % 100)
+        env.set_rk_counters(seed_ev, 7)
+        assert env.finished_count() == 7 * n and env.eval_count() == n * seed_ev
+        for t in range(T):
+            env.step(torch.full((n, env.action_dim), 0.3, dtype=torch.float64, device=env.device))
+        runs.append((env.eval_count(), env.finished_count()))
+        env.close()
+    (ev0, fin0), (ev1, fin1) = runs
+    assert fin0 == fin1 == (7 + T) * n, runs
+    assert ev0 > 50 * n                      # every env spent more than 50 evaluations: each low half wrapped once
+    assert ev1 == n * (2**32 - 50) + ev0 - n * 2**32, runs
