@@ -245,4 +245,14 @@ struct DState {
      * (bioim_eval_count), high 32 the env steps finished (bioim_finished_count);
      * one 64-bit update per launch */
     uint64_t *rkev;
+    /* the realize cache (step kernels of the planar muscle models, DESIGN.md
+     * 5.10): [N][cache_dim] per env, written by every realize for the next
+     * launch's first substep — the packed lower M + h C + h^2 K and the
+     * implicit right-hand side at that substep's h (the state does not change
+     * between the realize and that substep; muscle forces do not depend on
+     * the excitations), per muscle the fiber-velocity root, dv/dl and the
+     * clamp flag, then that h; valid[N] = 1 when the row belongs to the
+     * current state (every other writer of the state clears it) */
+    Real *cache;
+    int32_t *cache_ok;
 };

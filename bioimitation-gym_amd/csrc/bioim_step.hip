@@ -441,6 +441,21 @@ DEV void sincos_rt(double x, double &s, double &c) {
 DEV void sincos_rt(float x, float &s, float &c) { sincosf(x, &s, &c); }
 
 /* ----------------------------------------------------- smooth curves */
+/* BIOIM_EXACT_RCP=1: a diagnostic build (never shipped) whose reciprocals
+ * and inverse square roots below are IEEE divisions and square roots, the
+ * oracle's operations — to attribute the GPU's operation-level distance from
+ * the oracle */
+#ifndef BIOIM_EXACT_RCP
+#define BIOIM_EXACT_RCP 0
+#endif
+#if BIOIM_EXACT_RCP
+DEV double newton_rcp(double x) { return 1.0 / x; }
+DEV float newton_rcp(float x) { return 1.0f / x; }
+DEV double fast_rcp(double x) { return 1.0 / x; }
+DEV float fast_rcp(float x) { return 1.0f / x; }
+DEV double fast_rsqrt(double x) { return 1.0 / sqrt(x); }
+DEV float fast_rsqrt(float x) { return 1.0f / sqrtf(x); }
+#else
 /* reciprocal for Newton updates (a self-correcting iteration tolerates a
  * last-bits error in the step): hardware rcp plus one refinement */
 DEV double newton_rcp(double x) {
@@ -477,6 +492,7 @@ DEV float fast_rsqrt(float x) {
     float y = __builtin_amdgcn_rsqf(x);
     return fmaf(y, fmaf(-0.5f * x * y, y, 0.5f), y);
 }
+#endif
 
 /* a quintic segment in the power basis c[0] + c[1] u + ... + c[5] u^5
  * (converted from the Bezier control points at create time, convert_curve):
@@ -722,6 +738,35 @@ template <class T, typename Real> struct Lay {
      * the other env of a 32-lane group hits (ds_read_b64: 2 x 32 lanes;
      * ds_read_b128: 16-lane groups mixing both envs) */
     static constexpr int SIZE = (BIOIM_ENV_MOD >= 0 && T::PLANAR) ? SIZE0 + ((BIOIM_ENV_MOD - SIZE0 % 32) + 32) % 32 : SIZE0;
+};
+
+/* The realize cache (DState::cache): a step's realize runs at
+ * the state the next step's first substep starts from, and a muscle model's
+ * forces there do not depend on the excitations the policy sends next (they
+ * enter only the activation rate).  So the realize also forms the implicit
+ * system of that substep (h = the next step's substep length: M + h C + h^2 K
+ * and its right-hand side, CJ / LIM at that h) and the muscles' fiber-velocity
+ * roots, and stores them per env; the next launch's first substep loads them
+ * and goes straight to the solve instead of a whole dynamics call.  Torque
+ * models (the actuator torques are the controls) and the spatial models
+ * (register budget) run every substep in full. */
+#ifndef BIOIM_REALIZE_CACHE
+#define BIOIM_REALIZE_CACHE 1
+#endif
+#ifndef BIOIM_REALIZE_CACHE_SPATIAL
+#define BIOIM_REALIZE_CACHE_SPATIAL 1
+#endif
+template <class T> struct CacheLay {
+    static constexpr bool ON = BIOIM_REALIZE_CACHE && T::NM > 0 && (T::PLANAR || BIOIM_REALIZE_CACHE_SPATIAL);
+    /* planar kernels load the row at kernel start, ahead of the action
+     * pre-processing; the spatial ones (no register headroom) at the substep */
+    static constexpr bool PREFETCH = T::PLANAR;
+    static constexpr int ND = T::ND > 0 ? T::ND : 1, NP = ND * (ND + 1) / 2;
+    static constexpr int SYS = NP + ND;          /* [NP] packed lower M(h), [ND] rhs(h): LDS MP..RHS order */
+    static constexpr int MUS = SYS;              /* [NM][3] fiber-velocity root, dv/dl, clamped (0 / 1) */
+    static constexpr int H = MUS + 3 * T::NM;    /* the h the system was formed at */
+    static constexpr int DIM = ON ? H + 1 : 0;
+    static constexpr int PF = (SYS + T::G - 1) / T::G;   /* system values per lane */
 };
 
 /* apply_perturbations kernels only: per env 5 doubles after all env regions
@@ -1416,6 +1461,23 @@ template <typename Real> struct MState {
     bool clamped;
 };
 
+/* activation rate du/dt = (u - a) / tau, tau = tau_act (0.5 + 1.5 a) or
+ * tau_deact / (0.5 + 1.5 a), a the clamped activation (muscle_eval; the
+ * cached first substep of CACHE kernels) */
+template <bool BF, typename Real> DEV Real act_rate(const SMuscle<Real> &mu, Real a, Real excitation) {
+    if constexpr (BF) {
+        const Real amin = mu.amin, one = 1;
+        Real u = excitation < amin ? amin : (excitation > one ? one : excitation);
+        const Real ab = Real(0.5) + Real(1.5) * a;
+        const Real da_act = (u - a) * fast_rcp(mu.tau_act * ab), da_deact = (u - a) * ab * fast_rcp(mu.tau_deact);
+        return u > a ? da_act : da_deact;
+    } else {
+        Real u = excitation < mu.amin ? mu.amin : (excitation > Real(1) ? Real(1) : excitation);
+        const Real ab = Real(0.5) + Real(1.5) * a;
+        return u > a ? (u - a) * fast_rcp(mu.tau_act * ab) : (u - a) * ab * fast_rcp(mu.tau_deact);
+    }
+}
+
 template <bool BFK, bool BFC, class T, typename Real>
 DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_state, Real l_state, Real excitation,
                      Real L, Real v_warm, MState<Real> &s) {
@@ -1493,17 +1555,10 @@ DEV void muscle_eval(const SModel<T, Real> &SM, const SMuscle<Real> &mu, Real a_
     if constexpr (BF) {
         const Real dvdl = -(dGdl * fast_rcp(dGdv)) * mu.lv;
         s.dvdl = clamped ? zero : dvdl;
-        Real u = excitation < amin ? amin : (excitation > one ? one : excitation);
-        const Real ab = Real(0.5) + Real(1.5) * a;
-        /* du/dt = (u - a) / tau, tau = tau_act (0.5 + 1.5 a) or tau_deact / (0.5 + 1.5 a) */
-        const Real da_act = (u - a) * fast_rcp(mu.tau_act * ab), da_deact = (u - a) * ab * fast_rcp(mu.tau_deact);
-        s.dadt = u > a ? da_act : da_deact;
     } else {
         s.dvdl = clamped ? Real(0) : -(dGdl * fast_rcp(dGdv)) * mu.lv;
-        Real u = excitation < mu.amin ? mu.amin : (excitation > Real(1) ? Real(1) : excitation);
-        const Real ab = Real(0.5) + Real(1.5) * a;
-        s.dadt = u > a ? (u - a) * fast_rcp(mu.tau_act * ab) : (u - a) * ab * fast_rcp(mu.tau_deact);
     }
+    s.dadt = act_rate<BF>(mu, a, excitation);
     STAMP(18);
 }
 
@@ -1732,14 +1787,40 @@ DEV Real pert_force(const PertArgs<Real> &P, double *sl, int k) {
  * Lane d < ND owns dof d (qd, ud in, D.qdd out); lane's j-th muscle is
  * m = lane + j*G.  h > 0: increment of the linearly-implicit substep;
  * h == 0: the true accelerations (realize).  Leaves coordinates, frames,
- * contact wrenches, limit forces and q'' (RHS slots) published in LDS. */
-template <class T, typename Real, bool PERT, bool BF_ROWS, bool IMP>
+ * contact wrenches, limit forces and q'' (RHS slots) published in LDS.
+ * CACHE kernels (CacheLay): CI.make — a realize also forms the implicit
+ * system at h = CI.hc and stores it with the fiber-velocity roots into the
+ * env's cache row (CI.row()); CI.use — a first substep takes its system and
+ * roots from the cache (CI.sys / CI.mus, loaded at kernel start) and only
+ * solves: the state is the one the last realize ran at. */
+template <class T, typename Real> struct CacheIO {
+    static constexpr int PF = CacheLay<T>::PF > 0 ? CacheLay<T>::PF : 1;
+    static constexpr int PFA = CacheLay<T>::PREFETCH ? PF : 1, MPA = CacheLay<T>::PREFETCH ? Lay<T, Real>::MPL : 1;
+    bool use = false, make = false;
+    Real hc = 0;
+    /* this env's row, formed at each use from the uniform base and an opaque
+     * copy of the env index: a row address kept live through the kernel was
+     * split by the register allocator into lane-divergent AGPR copies in the
+     * fused C5 kernel (tools/hazard_gate.py) */
+    Real *base = nullptr;
+    int env = 0, N = 0;
+    DEV Real *row() const {
+        int e = env;
+        asm volatile("" : "+v"(e));
+        return base + GIDX((size_t)e * CacheLay<T>::DIM, (size_t)N * CacheLay<T>::DIM);
+    }
+    Real sys[PFA];     /* PREFETCH: the row's system values k = lane + i G */
+    Real mus[MPA][3];  /* PREFETCH: this lane's muscles' root, dv/dl, clamp flag */
+};
+
+template <class T, typename Real, bool PERT, bool BF_ROWS, bool IMP, bool CACHE = false>
 DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Real ud,
                   const Real (&act)[Lay<T, Real>::MPL], const Real (&lce)[Lay<T, Real>::MPL],
                   const Real (&control)[Lay<T, Real>::MPL], int lane, Real *lds, Real h, bool equilibrate,
-                  const PertArgs<Real> &P, double *pslot, int pk, Dyn<T, Real> &D) {
+                  const PertArgs<Real> &P, double *pslot, int pk, Dyn<T, Real> &D, const CacheIO<T, Real> &CI) {
     using LY = Lay<T, Real>;
     constexpr int ND = LY::ND, NP = LY::NP, NB = T::NB, G = T::G, MPL = LY::MPL;
+    static_assert(!CACHE || (CacheLay<T>::ON && IMP && !PERT), "the realize cache: semi-implicit planar muscle kernels");
     static_assert(NB < G && ND <= G, "lane NB writes the ground slot; one lane per dof");
     /* the semi-implicit planar kernels: the implicit contact / limit terms
      * without a branch on h (the spatial kernels keep it: register budget) */
@@ -1766,6 +1847,43 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
      * profiles/r03/r03k, r03l) */
     constexpr bool BFC = true;
     STAMP_DECL
+    if (CACHE && CI.use) {
+        /* the first substep of a launch from the last realize's cache: the
+         * implicit system at this h into MP..RHS, the muscles' roots, and the
+         * activation rates at this step's excitations */
+        using CL = CacheLay<T>;
+        Real *const crow = CL::PREFETCH ? nullptr : CI.row();
+#pragma unroll
+        for (int i = 0; i < CacheIO<T, Real>::PF; ++i)
+            if (lane + i * G < CL::SYS) {
+                if constexpr (CL::PREFETCH) lds[LY::MP + lane + i * G] = CI.sys[i];
+                else lds[LY::MP + lane + i * G] = GAT(crow, lane + i * G, CL::DIM);
+            }
+        if constexpr (T::NM > 0) {
+#pragma unroll
+            for (int j = 0; j < MPL; ++j) {
+                const int m = mslot<T>(lane + j * G);
+                if (m < T::NM) {
+                    const SMuscle<Real> &mu = SM.mus[m];
+                    const Real amin = mu.amin, one = 1, a_state = act[j];
+                    const Real a = a_state < amin ? amin : (a_state > one ? one : a_state);
+                    MState<Real> &s = D.ms[j];
+                    Real cv[3];
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        if constexpr (CL::PREFETCH) cv[c] = CI.mus[j][c];
+                        else cv[c] = GAT(crow, CL::MUS + 3 * m + c, CL::DIM);
+                    }
+                    s.vN = cv[0];
+                    s.vce = s.vN * mu.lv;
+                    s.dvdl = cv[1];
+                    s.clamped = cv[2] != Real(0);
+                    s.dadt = act_rate<BFK_ME>(mu, a, control[j]);
+                }
+            }
+        }
+        wave_sync();
+    } else {
     publish_coords<T, Real>(M, SM, lds, lane, qd, ud);
     if (lane < ND) {
 #pragma unroll
@@ -1845,6 +1963,9 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
         }
     }
     STAMP(3);
+    /* the implicit terms' h: a CACHE realize forms them at the next step's
+     * substep length (its explicit q'' below does not use them) */
+    const Real hi = (CACHE && CI.make) ? CI.hc : h;
     /* contacts computed by the first muscle pass when every sphere lane
      * holds a muscle there */
     constexpr bool MUSCLE_CONTACT = T::NM >= T::NS && T::NS > 0;
@@ -1874,7 +1995,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
                 /* the sphere contacts ride in the first muscle pass (every
                  * sphere lane holds a muscle): same block as the curve
                  * evaluations, so their chains interleave */
-                if constexpr (j == 0 && MUSCLE_CONTACT) contact_compute<BFK_CON, T, Real>(SM, lds, lane < T::NS ? lane : 0, h, CO);
+                if constexpr (j == 0 && MUSCLE_CONTACT) contact_compute<BFK_CON, T, Real>(SM, lds, lane < T::NS ? lane : 0, hi, CO);
                 muscle_eval<BFK_ME, BFC, T, Real>(SM, mu, a_, l_, control[j], L, D.ms[j].vN, D.ms[j]);
                 const Real nFt = -D.ms[j].Ft;
                 Real *ts = lds + LY::TAU + (lane + j * G) * T::MAXSPAN;
@@ -1895,7 +2016,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
     if constexpr (MUSCLE_CONTACT) {
         if (lane < T::NS) contact_store<T, Real>(lds, lane, CO);
     } else {
-        if (lane < T::NS) contact_lane<BFK_CON, T, Real>(SM, lds, lane, h);
+        if (lane < T::NS) contact_lane<BFK_CON, T, Real>(SM, lds, lane, hi);
     }
     STAMP(6);
     if (lane < T::NL) {
@@ -1906,13 +2027,13 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
         Real lo = smooth_step<BFK_LIM>(Real(1), Real(0), qlo - tr, qlo, itr, qv);
         Real f = -SM.lim_kup[lane] * up * (qv - qup) + SM.lim_klow[lane] * lo * (qlo - qv) - SM.lim_damp[lane] * (up + lo) * qd;
         Real diag = 0, tadd = f;
-        if (IMP_BF || (!IMP_BF && h > 0)) {   /* IMP_BF: no branch on h (at h = 0 this gives diag = 0, tadd = f) */
+        if (IMP_BF || (!IMP_BF && hi > 0)) {   /* IMP_BF: no branch on h (at h = 0 this gives diag = 0, tadd = f) */
             Real dup = smooth_step_d<BFK_LIM>(Real(0), Real(1), qup, qup + tr, itr, qv);
             Real dlo = smooth_step_d<BFK_LIM>(Real(1), Real(0), qlo - tr, qlo, itr, qv);
             Real kq = SM.lim_kup[lane] * (up + dup * (qv - qup)) + SM.lim_klow[lane] * (lo - dlo * (qlo - qv));
             Real cq = SM.lim_damp[lane] * (up + lo);
-            diag = h * cq + h * h * kq;
-            tadd = f - h * kq * qd;
+            diag = hi * cq + hi * hi * kq;
+            tadd = f - hi * kq * qd;
         }
         Real *lm = lds + LY::LIM + 4 * lane;
         lm[0] = f; lm[1] = diag; lm[2] = tadd;
@@ -1933,9 +2054,15 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
      * M_kl = S_l . G_k (every l on k's path moves the spheres k moves).  All
      * inputs (S, IC, CJ, LIM) were published before the last sync, so the
      * row needs no exchange between lanes. */
-    const bool implicit = h > 0;
+    const bool implicit = hi > 0;
     using PL = Planar<T>;
     constexpr unsigned ZW = PL::ZW, ZV = PL::ZV;
+    /* EX: the explicit system of a CACHE realize (h = 0: the contact force
+     * without its implicit correction — the CW slot — the limit forces, no
+     * implicit blocks), after its implicit one went to the cache; otherwise
+     * the system at hi */
+    auto phase3 = [&](auto EXc) {
+    constexpr bool EX = decltype(EXc)::value;
     if (lane < ND) {
         Real Sd[6];
 #pragma unroll
@@ -1961,6 +2088,9 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
             constexpr int sp = decltype(sI)::value;
             constexpr unsigned msk = T::dofmask[T::sphere_cb[sp]];
             const Real *cj = lds + LY::CJ + LY::CJN * sp, *C = cj + 6;
+            /* the force: CW (= F where the sphere is active, 0 elsewhere, so
+             * on * F alike) for the explicit system */
+            const Real *Fs = EX ? lds + LY::CW + 8 * sp : cj + 3;
             Real jd[3];
             cross3m<ZW, 0>(Sd, cj, jd);
 #pragma unroll
@@ -1971,11 +2101,11 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
              * branch, two basic blocks per sphere */
             const bool onb = lds[LY::CW + 8 * sp + 6] > 0 && ((msk >> lane) & 1u);
             const Real on = onb ? Real(1) : Real(0);
-            if constexpr (BFK_ROW) r = fma(on, dot3m<ZV, 0>(jd, cj + 3), r);
-            else r += onb ? dot3m<ZV, 0>(jd, cj + 3) : Real(0);
+            if constexpr (BFK_ROW) r = fma(on, dot3m<ZV, 0>(jd, Fs), r);
+            else r += onb ? dot3m<ZV, 0>(jd, Fs) : Real(0);
             /* IMP (the semi-implicit kernels): no branch on h — a realize
              * call (h = 0) has C = 0 (contact_compute), adding zeros */
-            if (IMP_BF || (!IMP_BF && implicit)) {
+            if (!EX && (IMP_BF || (!IMP_BF && implicit))) {
                 Real w[3] = {(ZV & 4u) ? C[0] * jd[0] : C[0] * jd[0] + C[1] * jd[2], C[2] * jd[1],
                              C[1] * jd[0] + C[3] * jd[2]};
                 Real pw[3];
@@ -1996,8 +2126,8 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
 #pragma unroll
         for (int li = 0; li < T::NL; ++li) {   /* selects: no per-limit branch */
             const bool mine = SM.lim_dof[li] == lane;
-            r += mine ? lds[LY::LIM + 4 * li + 2] : Real(0);
-            dg += mine ? lds[LY::LIM + 4 * li + 1] : Real(0);
+            r += mine ? lds[LY::LIM + 4 * li + (EX ? 0 : 2)] : Real(0);
+            if constexpr (!EX) dg += mine ? lds[LY::LIM + 4 * li + 1] : Real(0);
         }
         lds[LY::RHS + lane] = r;
         /* Row k's entries (k, l), l <= k.  BF_ROWS: branch-free, every l is
@@ -2025,13 +2155,38 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
                 for (int i = 0; i < 6; ++i) Sl[i] = lds[LY::S + 6 * l + i];
                 PL::col(Sl);
                 Real v = dot3m<ZW, 0>(Sl, Gk) + dot3m<ZV, 0>(Sl + 3, Gk + 3);
-                return v + (implicit && l == lane ? dg : Real(0));
+                return EX ? v : v + (implicit && l == lane ? dg : Real(0));
             };
             if constexpr (BF_ROWS) row[l <= lane ? l : 0] = entry();
             else if ((path >> l) & 1u) row[l] = entry();
         });
     }
+    };
+    phase3(std::integral_constant<bool, false>{});
     wave_sync();
+    if constexpr (CACHE) {
+        if (CI.make) {
+            /* the implicit system at hi for the next launch's first substep, then
+             * this realize's explicit one over it */
+            using CL = CacheLay<T>;
+            Real *const crow = CI.row();
+            for (int k = lane; k < CL::SYS; k += G) GAT(crow, k, CL::DIM) = lds[LY::MP + k];
+            if (lane == 0) GAT(crow, CL::H, CL::DIM) = hi;
+#pragma unroll
+            for (int j = 0; j < MPL; ++j) {
+                const int m = mslot<T>(lane + j * G);
+                if (m < T::NM) {
+                    GAT(crow, CL::MUS + 3 * m, CL::DIM) = D.ms[j].vN;
+                    GAT(crow, CL::MUS + 3 * m + 1, CL::DIM) = D.ms[j].dvdl;
+                    GAT(crow, CL::MUS + 3 * m + 2, CL::DIM) = D.ms[j].clamped ? Real(1) : Real(0);
+                }
+            }
+            wave_sync();
+            phase3(std::integral_constant<bool, true>{});
+            wave_sync();
+        }
+    }
+    }   /* phases 0-3 (not a cached first substep) */
     STAMP(8);
 
     /* ---- phase 4: tree-sparse LTL solve (ltl_solve), redundant in every
@@ -2663,6 +2818,32 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             if (osim) control[j] = GAT(st.ctl, (size_t)m * N + env, (size_t)NA * N);
         }
     }
+    /* the realize cache (CacheLay): a step's first substep takes its system
+     * from the last launch's realize when that row is valid for this state
+     * and was formed at this step's substep length (checked below); loaded
+     * here, ahead of the action pre-processing */
+    constexpr bool CACHE = CacheLay<T>::ON && !PERT && !RK && !REP;
+    CacheIO<T, Real> CI;
+    bool cache_valid = false;
+    Real cache_h = 0;
+    if constexpr (CACHE) {
+        using CL = CacheLay<T>;
+        CI.base = st.cache; CI.env = env; CI.N = N;
+        Real *const crow = st.cache + GIDX((size_t)env * CL::DIM, (size_t)N * CL::DIM);
+        cache_valid = mode == 0 && GAT(st.cache_ok, env, (size_t)N) != 0;
+        cache_h = GAT(crow, CL::H, CL::DIM);
+        if constexpr (CL::PREFETCH) {
+#pragma unroll
+            for (int i = 0; i < CacheIO<T, Real>::PF; ++i)
+                CI.sys[i] = lane + i * G < CL::SYS ? GAT(crow, lane + i * G, CL::DIM) : Real(0);
+#pragma unroll
+            for (int j = 0; j < MPL; ++j) {
+                const int m = mslot<T>(lane + j * G);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) CI.mus[j][c] = m < NM ? GAT(crow, CL::MUS + 3 * m + c, CL::DIM) : Real(0);
+            }
+        }
+    }
     int done = 0;
     Real rew = 0, inf[5] = {0, 0, 0, 0, 0};
     bool do_reset = (mode == 1);
@@ -2885,8 +3066,25 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                 control[j] = m < NA ? GAT(st.ctl, (size_t)m * N + env, (size_t)NA * N) : Real(0);
                 if constexpr (NM > 0)
                     if (m < NM) act[j] = SM.mus[m].default_act;
+                /* CACHE: the reset realize's fiber-velocity roots start cold,
+                 * as the reset table's do (build_reset_table), so the cache row
+                 * it leaves is the table's bit for bit */
+                if constexpr (CACHE) D.ms[j].vN = 0;
             }
             resets += 1;
+        }
+        if constexpr (CACHE) {
+            /* the first substep from the cache; a realize (step or reset) forms
+             * the cache at the next step's substep length (begin_integrate's
+             * arithmetic for istep + 1) */
+            CI.use = cache_valid && sub && remaining == M.nsub && cache_h == dt;
+            cache_valid = false;
+            CI.make = !sub;
+            if (!sub) {
+                const double tf = M.step_size * (double)(istep + 1);
+                const double hstep = tf - t;
+                CI.hc = Real(hstep / (double)M.nsub);
+            }
         }
         {
             /* opaque per-iteration model pointer: keeps the compiler from
@@ -2914,9 +3112,9 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             /* RK: explicit accelerations (h = 0, the implicit terms compile away) */
             /* branch-free phase-3 row stores, except in the spatial RK kernels
              * (they would take those kernels past the 512-register budget) */
-            dynamics<T, Real, PERT, !RK || T::PLANAR, !RK>(*(const DModel<Real> *)Mi, SM, qd, ud, act, lce, control, lane, lds,
+            dynamics<T, Real, PERT, !RK || T::PLANAR, !RK, CACHE>(*(const DModel<Real> *)Mi, SM, qd, ud, act, lce, control, lane, lds,
                                     RK ? Real(0) : (sub ? dt : Real(0)), eq && NM > 0, PA, pslot,
-                                    RK ? 0 : M.nsub - remaining, D);
+                                    RK ? 0 : M.nsub - remaining, D, CI);
         }
         if (RK && sub) {
             const Real h = Real(rk_h);
@@ -3301,6 +3499,12 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                         if (obs)
                             for (int k = lane; k < M.obs_dim; k += G)
                                 GAT(obs, (size_t)env * a.obs_stride + k, (size_t)N * a.obs_stride) = tr[NM + k];
+                        if constexpr (CACHE) {   /* the row's realize cache (after its observation) */
+                            using CL = CacheLay<T>;
+                            const Real *tc = tr + NM + M.obs_dim;
+                            Real *const crow = CI.row();
+                            for (int k = lane; k < CL::DIM; k += G) GAT(crow, k, CL::DIM) = tc[k];
+                        }
                     } else {
                         /* the held torques per dof, gathered as in the dynamics
                          * call (TAU slots, SM.tau_src), then q'' per dof lane */
@@ -3357,6 +3561,13 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             GAT(st.resets, env, (size_t)N) = resets;
         }
         if (RK || mode == 1 || (osim && a.osim_op == BIOIM_OSIM_EQUILIBRATE)) GAT(st.hrk, env, (size_t)N) = rk_hnext;
+        /* the realize cache: every step or reset of a CACHE kernel ends with a
+         * realize (or a reset-table row) that formed this env's row.  The other
+         * kernels of such a topology (push, RK, OsimModel calls) change the
+         * state without it: the host clears the flags before launching them
+         * (launch_impl; a store here cost the spatial push + RK kernel its
+         * last registers) */
+        if constexpr (CACHE) GAT(st.cache_ok, env, (size_t)N) = 1;
         if constexpr (RK) {
             GAT(st.pend, env, (size_t)N) = suspend ? 1 : 0;
             /* evaluations (low 32 bits): the attempts', plus one realize per
@@ -3828,6 +4039,7 @@ struct Ops {
     const char *topo;   /* the topology struct's name (fused-pair lookup) */
     int lanes;
     size_t lds_bytes;   /* per workgroup: model image + BIOIM_EPB env regions */
+    int cache_dim;      /* reals per env of the realize cache (CacheLay<T>::DIM; 0: none) */
     int (*upload)(bioim_handle_t *);
     void (*launch)(bioim_handle_t *, int mode, const void *actions, void *obs, void *reward, uint8_t *done, void *info,
                    const int32_t *env_ids, const int32_t *ref_index, int n_list, const OsimCall *oc);
@@ -3863,6 +4075,7 @@ struct bioim_handle {
     void *reset_tab;      /* Real [pack.nrows][reset_table_dim] or null (build_reset_table) */
     int planar;           /* the pack's topology is planar (pack_is_planar) */
     int reset_tab_on;     /* bioim_set_reset_table (default 1) */
+    int cache_live;       /* a default step kernel ran since the realize-cache flags were last cleared */
     Ops ops;
     bioim_modelpack_t pack;
 };
@@ -3875,10 +4088,13 @@ static inline bool reset_table_wanted(const bioim_handle_t *h) {
            !h->force_out && !h->traj;
 }
 static inline bool reset_table_eligible(const bioim_handle_t *h) { return h->reset_tab && reset_table_wanted(h); }
-/* reals per table row: muscle models [nmuscle fiber lengths][obs]; torque
- * models [ndof x ndof M^-1, row-major][obs at zero held torques] */
+/* reals per env of the realize cache (CacheLay) */
+static inline int cache_dim(const bioim_handle_t *h) { return h->ops.cache_dim; }
+/* reals per table row: muscle models [nmuscle fiber lengths][obs][the reset
+ * realize's cache row, CacheLay]; torque models [ndof x ndof M^-1,
+ * row-major][obs at zero held torques] */
 static inline int reset_table_dim(const bioim_handle_t *h) {
-    return (h->nmuscle > 0 ? h->nmuscle : h->ndof * h->ndof) + h->obs_dim;
+    return (h->nmuscle > 0 ? h->nmuscle : h->ndof * h->ndof) + h->obs_dim + (h->nmuscle > 0 ? cache_dim(h) : 0);
 }
 
 namespace {
@@ -3946,6 +4162,18 @@ void launch_impl(bioim_handle_t *h, int mode, const void *actions, void *obs, vo
      * kernels' code is untouched by the (rarely used) push */
     constexpr size_t lds0 = lds_bytes<T, Real, false>(), lds1 = lds_bytes<T, Real, true>();
     const dim3 g(a.blocks), b(BIOIM_EPB * T::G);
+    /* the realize cache (CacheLay): only the default step kernels form and
+     * read it; before any other kernel changes the state, every env's row is
+     * marked stale (once per switch: cache_live says a default launch may
+     * have set flags since) */
+    const bool default_kernel = mode != 2 && a.pert_n == 0 && !h->rk;
+    if constexpr (CacheLay<T>::ON) {
+        if (!default_kernel && h->cache_live) {
+            hipMemsetAsync(a.st.cache_ok, 0, sizeof(int32_t) * (size_t)h->n, h->stream);
+            h->cache_live = 0;
+        }
+        if (default_kernel) h->cache_live = 1;
+    }
     if (mode == 2) {   /* OsimModel calls: the REP kernels */
         if (a.pert_n > 0 && h->rk) hipLaunchKernelGGL((env_kernel<T, Real, true, true, true>), g, b, lds1, h->stream, a);
         else if (a.pert_n > 0) hipLaunchKernelGGL((env_kernel<T, Real, true, false, true>), g, b, lds1, h->stream, a);
@@ -3984,6 +4212,7 @@ int fused_launch_impl(bioim_handle_t *h0, bioim_handle_t *h1, const void *action
         if (dev >= 0 && dev < 64) attr[dev] = true;
     }
     if (a0.blocks + a1.blocks <= 0) return 0;
+    h0->cache_live = 1; h1->cache_live = 1;   /* default step kernels: they form the realize cache */
     hipLaunchKernelGGL((env_kernel2<T0, T1, Real>), dim3(a0.blocks + a1.blocks), dim3(BIOIM_EPB * T0::G), lds,
                        h0->stream, a0, a1);
     return 0;
@@ -4036,6 +4265,7 @@ template <class T> bool pick(const bioim_modelpack_t &p, int precision, Ops &ops
     if (p.obs_dim > Lay<T, double>::OBSMAX) return false;
     ops.topo = name;
     ops.lanes = T::G;
+    ops.cache_dim = CacheLay<T>::DIM;
     if (precision == 64) {
         ops.launch = &launch_impl<T, double>;
         ops.id_launch = &id_launch_impl<T, double>;
@@ -4068,6 +4298,7 @@ template <typename Real> size_t state_layout(bioim_handle_t *h, char *base, DSta
            ora = take(sizeof(int32_t) * n), octl = take(sizeof(Real) * na1 * n), ocur = take(sizeof(Real) * na1 * n),
            ovn = take(sizeof(Real) * nm1 * n);
     size_t oev = take(sizeof(uint64_t) * n);
+    size_t occ = take(sizeof(Real) * (size_t)cache_dim(h) * n), ocv = take(sizeof(int32_t) * n);
     if (st) {
         st->q = (Real *)(base + oq); st->u = (Real *)(base + ou); st->act = (Real *)(base + oa);
         st->lce = (Real *)(base + ol); st->hist = (Real *)(base + oh); st->last = (Real *)(base + olast);
@@ -4078,6 +4309,7 @@ template <typename Real> size_t state_layout(bioim_handle_t *h, char *base, DSta
         st->rka = (int32_t *)(base + ora); st->ctl = (Real *)(base + octl); st->cur = (Real *)(base + ocur);
         st->vnw = (Real *)(base + ovn);
         st->rkev = (uint64_t *)(base + oev);
+        st->cache = (Real *)(base + occ); st->cache_ok = (int32_t *)(base + ocv);
     }
     return off;
 }
@@ -4144,6 +4376,7 @@ template <typename Real> int xfer_state(bioim_handle_t *h, double *host, const d
             hs.hrk[e] = s[k++];
             for (int i = 0; i < na; ++i) hs.ctl[i * n + e] = (Real)s[k++];
             hs.pend[e] = 0;   /* a state set from outside is at a step boundary */
+            hs.cache_ok[e] = 0;   /* the realize cache belongs to the state it was formed at */
         }
     }
     if (in) HIPCHK(hipMemcpy(h->state_buf, buf.data(), h->state_bytes, hipMemcpyHostToDevice));
@@ -4229,7 +4462,7 @@ int bioim_create(const bioim_modelpack_t *pack, int n_envs, int device, int prec
     h->obs_dim = pack->obs_dim; h->info_dim = pack->info_dim; h->nsub = pack->nsub; h->auto_reset = 0;
     h->env_offset = 0;
     h->pert_n = 0; h->pert_ob = -1;
-    h->reset_tab = nullptr; h->reset_tab_on = 1;
+    h->reset_tab = nullptr; h->reset_tab_on = 1; h->cache_live = 0;
     h->planar = pack_is_planar(*pack) ? 1 : 0;
     h->act_stride = pack->nact; h->obs_stride = pack->obs_dim; h->info_stride = pack->info_dim;
     h->ops = ops;
@@ -4295,7 +4528,9 @@ int bioim_reset(bioim_handle_t *h, const int32_t *env_ids, const int32_t *ref_in
  * scratch handle's held controls are 0) and M^-1 at the row's coordinates. */
 static int build_reset_table(bioim_handle_t *h) {
     const int nr = h->pack.nrows, nm = h->nmuscle, od = h->obs_dim, nd = h->ndof;
-    const size_t R = h->precision == 64 ? 8 : 4, head = nm > 0 ? (size_t)nm : (size_t)nd * nd, dim = head + od;
+    const size_t R = h->precision == 64 ? 8 : 4, head = nm > 0 ? (size_t)nm : (size_t)nd * nd;
+    const int cdim = nm > 0 ? cache_dim(h) : 0;
+    const size_t dim = head + od + cdim;   /* = reset_table_dim(h) */
     bioim_handle_t *tmp = nullptr;
     int rc = bioim_create(&h->pack, nr, h->device, h->precision, h->seed, &tmp);
     if (rc) return rc;
@@ -4359,6 +4594,15 @@ static int build_reset_table(bioim_handle_t *h) {
     }
     for (int r = 0; r < nr; ++r)
         memcpy(tab.data() + ((size_t)r * dim + head) * R, obs.data() + (size_t)r * od * R, (size_t)od * R);
+    if (cdim > 0) {   /* the reset realize's cache rows (DState::cache, [nr][cdim]) */
+        const DState<double> &ts = *reinterpret_cast<const DState<double> *>(tmp->dstate);
+        const size_t cb = (size_t)nr * cdim * R;
+        std::vector<unsigned char> crow(cb);
+        if (hipMemcpy(crow.data(), ts.cache, cb, hipMemcpyDeviceToHost) != hipSuccess)
+            return done(fail(BIOIM_E_DEVICE, "build_reset_table: cache rows failed"));
+        for (int r = 0; r < nr; ++r)
+            memcpy(tab.data() + ((size_t)r * dim + head + od) * R, crow.data() + (size_t)r * cdim * R, (size_t)cdim * R);
+    }
     if (hipMemcpy(d_tab, tab.data(), tab.size(), hipMemcpyHostToDevice) != hipSuccess)
         return done(fail(BIOIM_E_DEVICE, "build_reset_table: upload failed"));
     h->reset_tab = d_tab;

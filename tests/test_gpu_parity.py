@@ -855,6 +855,7 @@ def test_parity_200_steps_muscle_tracking_drive(env_id):
     limit_end = np.zeros(n, bool)                # ended by istep >= N on the oracle (and, by `done` equality, the GPU)
     e_gpu, e_twin = np.zeros((T, n)), np.zeros((T, n))
     seen = np.zeros((T, n), bool)
+    e_col = np.full((T, n), -1, int)        # the column of the GPU error (-1: reward)
     for t in range(T):
         acts = np.stack([drive(orc.get_state(bufs, i), sched[i, t // P]) for i in range(n)])
         obs, rew, done = (v.cpu().numpy() for v in env.step(torch.as_tensor(acts, device=env.device))[:3])
@@ -867,7 +868,9 @@ def test_parity_200_steps_muscle_tracking_drive(env_id):
                 dt = dt or d2
             if live[i]:
                 seen[t, i] = True
-                e_gpu[t, i] = max(_rel(obs[i], o).max(), abs(rew[i] - r) / max(1.0, abs(r)))
+                eo = _rel(obs[i], o)
+                e_gpu[t, i] = max(eo.max(), abs(rew[i] - r) / max(1.0, abs(r)))
+                e_col[t, i] = int(eo.argmax()) if eo.max() >= abs(rew[i] - r) / max(1.0, abs(r)) else -1
                 assert bool(done[i]) == d, (t, i)
             if d and orc_alive[i] and orc.get_state(bufs, i)[1] >= pk.n_episode:
                 limit_end[i] = True
@@ -878,6 +881,19 @@ def test_parity_200_steps_muscle_tracking_drive(env_id):
     eg, et = np.where(seen, e_gpu, 0).max(1), np.where(seen, e_twin, 0).max(1)
     ks = [0, 49, 99, 149, 199]
     ratio = np.where(seen, e_gpu / np.maximum(1e-30, e_twin), 0)
+    # where the worst GPU/twin ratio sits (step, env, column) and the worst
+    # ratio among env-steps whose GPU error is above the 1e-9 level of the one-step parity tests
+    from bioimitation.obslayout import column_names
+    names = column_names(pk, load_names(env_id))
+    wt, wi = np.unravel_index(int(ratio.argmax()), ratio.shape)
+    wc = int(e_col[wt, wi])
+    big = seen & (e_gpu > 1e-9)
+    rbig = np.where(big, ratio, 0)
+    bt, bi = np.unravel_index(int(rbig.argmax()), rbig.shape)
+    print(f'{env_id}: worst GPU/twin ratio {ratio[wt, wi]:.1f} at step {wt + 1} env {wi} row {int(rows[wi])} column '
+          f'{names[wc] if wc >= 0 else "reward"} (GPU {e_gpu[wt, wi]:.1e}, twins {e_twin[wt, wi]:.1e}); among env-steps '
+          f'with GPU error > 1e-9 ({big.sum()} of {seen.sum()}): worst ratio {rbig[bt, bi]:.1f} at step {bt + 1} env {bi} '
+          f'column {names[int(e_col[bt, bi])] if e_col[bt, bi] >= 0 else "reward"} (GPU {e_gpu[bt, bi]:.1e}, twins {e_twin[bt, bi]:.1e})')
     print(f'{env_id} 200 steps, scheduled tracking drive, rows {[int(r) for r in rows]}: alive at t=200 oracle '
           f'{orc_alive.sum()}/{n}, GPU {gpu_alive.sum()}/{n}, ended at the episode limit {limit_end.sum()}; max over envs of the rel err GPU vs oracle / '
           f'oracle vs its one-ulp twins at t=' + ', '.join(f'{k + 1}: {eg[k]:.1e} / {et[k]:.1e}' for k in ks) +
