@@ -134,6 +134,7 @@ template <> struct Eps<float> {
     static constexpr float v_tol = 1e-7f;   /* normalized velocity         */
     static constexpr float l_tol = 1e-9f;   /* fiber length (m)            */
     static constexpr float l_stop = 1e-9f;  /* Newton step after which the length is converged */
+    static constexpr float h_stop = 0.0f;   /* fiber-equilibrium residual stop (off in fp32) */
     static constexpr int it_max = 24;
     static constexpr int curve_newton = 1; /* from the Hermite start: 5.9e-9 < fp32 rounding */
 };
@@ -145,6 +146,13 @@ template <> struct Eps<double> {
     static constexpr double v_tol = 1e-15;
     static constexpr double l_tol = 1e-15;
     static constexpr double l_stop = 1e-10;
+    /* the oracle's residual stop of the reset fiber equilibrium
+     * (oracle/bioim_oracle.c muscle_equilibrium, |H| < 1e-12): where the root is
+     * ill-conditioned (a tendon at its slack length: H nearly flat in l) the
+     * iterate that stop returns is the oracle's, instead of one converged
+     * further (round 6: Palsy3D tib_ant_r at reset row 46, 9.2e-12 apart;
+     * DESIGN.md 2) */
+    static constexpr double h_stop = 1e-12;
     static constexpr int it_max = 60;
     static constexpr int curve_newton = 2; /* from the Hermite start: 8.9e-16 */
 };
@@ -748,16 +756,22 @@ template <class T, typename Real> struct Lay {
  * and its right-hand side, CJ / LIM at that h) and the muscles' fiber-velocity
  * roots, and stores them per env; the next launch's first substep loads them
  * and goes straight to the solve instead of a whole dynamics call.  Torque
- * models (the actuator torques are the controls) and the spatial models
- * (register budget) run every substep in full. */
+ * models: the actuator torques are the controls, so their cached right-hand
+ * side stops short of them and the cached substep adds this step's. */
 #ifndef BIOIM_REALIZE_CACHE
 #define BIOIM_REALIZE_CACHE 1
 #endif
 #ifndef BIOIM_REALIZE_CACHE_SPATIAL
 #define BIOIM_REALIZE_CACHE_SPATIAL 1
 #endif
+#ifndef BIOIM_REALIZE_CACHE_TORQUE
+#define BIOIM_REALIZE_CACHE_TORQUE 1
+#endif
 template <class T> struct CacheLay {
-    static constexpr bool ON = BIOIM_REALIZE_CACHE && T::NM > 0 && (T::PLANAR || BIOIM_REALIZE_CACHE_SPATIAL);
+    /* torque models: the cached right-hand side leaves out the actuator
+     * torques (the controls), which the cached substep adds */
+    static constexpr bool ON = BIOIM_REALIZE_CACHE &&
+                               (T::NM > 0 ? (T::PLANAR || BIOIM_REALIZE_CACHE_SPATIAL) : BIOIM_REALIZE_CACHE_TORQUE);
     /* planar kernels load the row at kernel start, ahead of the action
      * pre-processing; the spatial ones (no register headroom) at the substep */
     static constexpr bool PREFETCH = T::PLANAR;
@@ -1591,6 +1605,9 @@ DEV Real muscle_equilibrium(const SModel<T, Real> &SM, const SMuscle<Real> &mu, 
         Real ln = l - H / dH;
         const bool newton = ln >= lo && ln <= hi;
         if (!newton) ln = Real(0.5) * (lo + hi);
+        /* the residual stop as a zero step (the l_tol exit below), not an
+         * exit of its own: the spatial RK kernels have no register to spare */
+        ln = fabs(H) < Eps<Real>::h_stop ? l : ln;
         Real dl = fabs(ln - l);
         l = ln;
         if (dl <= Eps<Real>::l_tol || (it >= 1 && dl <= Real(1e3) * Eps<Real>::l_tol && dl >= Real(0.5) * dprev)) break;
@@ -1881,6 +1898,22 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
                     s.dadt = act_rate<BFK_ME>(mu, a, control[j]);
                 }
             }
+        } else {
+            /* this step's actuator torques (as phase 2 stores them), added
+             * to the cached right-hand side in phase 3's order */
+            if (lane == 0) lds[LY::TAU + LY::TZ] = Real(0);
+            sfor<0, MPL>([&](auto jI) {
+                constexpr int j = decltype(jI)::value;
+                const int m = mslot<T>(lane + j * G);
+                if (m < T::NA) lds[LY::TAU + (lane + j * G) * T::MAXSPAN] = control[j] * SM.ca_opt[m];
+            });
+            wave_sync();
+            if (lane < ND) {
+                Real r = lds[LY::RHS + lane];
+#pragma unroll
+                for (int i = 0; i < T::MAXARM; ++i) r += lds[LY::TAU + SM.tau_src[lane][i]];
+                lds[LY::RHS + lane] = r;
+            }
         }
         wave_sync();
     } else {
@@ -2070,8 +2103,13 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
         PL::col(Sd);
         const Real *wb = lds + LY::WB + 6 * SM.dof_cb[lane];
         Real r = -(dot3m<ZW, 0>(Sd, wb) + dot3m<ZV, 0>(Sd + 3, wb + 3));
+        /* torque models with the realize cache: the actuator torques last
+         * (the cache keeps the sum before them) */
+        constexpr bool TAU_LAST = CACHE && T::NM == 0;
+        if constexpr (!TAU_LAST) {
 #pragma unroll
-        for (int i = 0; i < T::MAXARM; ++i) r += lds[LY::TAU + SM.tau_src[lane][i]];
+            for (int i = 0; i < T::MAXARM; ++i) r += lds[LY::TAU + SM.tau_src[lane][i]];
+        }
         Real Gk[6];
         {
             const Real *ic = lds + LY::IC + 10 * SM.dof_cb[lane];
@@ -2129,7 +2167,14 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
             r += mine ? lds[LY::LIM + 4 * li + (EX ? 0 : 2)] : Real(0);
             if constexpr (!EX) dg += mine ? lds[LY::LIM + 4 * li + 1] : Real(0);
         }
-        lds[LY::RHS + lane] = r;
+        if constexpr (TAU_LAST) {
+            Real rt = r;
+#pragma unroll
+            for (int i = 0; i < T::MAXARM; ++i) rt += lds[LY::TAU + SM.tau_src[lane][i]];
+            lds[LY::RHS + lane] = (!EX && CI.make) ? r : rt;   /* the cache's rhs: without the controls */
+        } else {
+            lds[LY::RHS + lane] = r;
+        }
         /* Row k's entries (k, l), l <= k.  BF_ROWS: branch-free, every l is
          * computed and stored in row k's own slots (those off k's root path
          * are structural zeros ltl_solve never reads); columns l > k (not in
@@ -3538,6 +3583,12 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
                         if (obs)
                             for (int k = lane; k < M.obs_dim; k += G)
                                 GAT(obs, (size_t)env * a.obs_stride + k, (size_t)N * a.obs_stride) = ob[k];
+                        if constexpr (CACHE) {   /* the row's realize cache (after its observation) */
+                            using CL = CacheLay<T>;
+                            const Real *tc = tr + NI + M.obs_dim;
+                            Real *const crow = CI.row();
+                            for (int k = lane; k < CL::DIM; k += G) GAT(crow, k, CL::DIM) = tc[k];
+                        }
                     }
                     break;
                 }
@@ -4090,11 +4141,11 @@ static inline bool reset_table_wanted(const bioim_handle_t *h) {
 static inline bool reset_table_eligible(const bioim_handle_t *h) { return h->reset_tab && reset_table_wanted(h); }
 /* reals per env of the realize cache (CacheLay) */
 static inline int cache_dim(const bioim_handle_t *h) { return h->ops.cache_dim; }
-/* reals per table row: muscle models [nmuscle fiber lengths][obs][the reset
- * realize's cache row, CacheLay]; torque models [ndof x ndof M^-1,
- * row-major][obs at zero held torques] */
+/* reals per table row: muscle models [nmuscle fiber lengths][obs]; torque
+ * models [ndof x ndof M^-1, row-major][obs at zero held torques]; then the
+ * reset realize's cache row (CacheLay; torque models: without the controls) */
 static inline int reset_table_dim(const bioim_handle_t *h) {
-    return (h->nmuscle > 0 ? h->nmuscle : h->ndof * h->ndof) + h->obs_dim + (h->nmuscle > 0 ? cache_dim(h) : 0);
+    return (h->nmuscle > 0 ? h->nmuscle : h->ndof * h->ndof) + h->obs_dim + cache_dim(h);
 }
 
 namespace {
@@ -4529,7 +4580,7 @@ int bioim_reset(bioim_handle_t *h, const int32_t *env_ids, const int32_t *ref_in
 static int build_reset_table(bioim_handle_t *h) {
     const int nr = h->pack.nrows, nm = h->nmuscle, od = h->obs_dim, nd = h->ndof;
     const size_t R = h->precision == 64 ? 8 : 4, head = nm > 0 ? (size_t)nm : (size_t)nd * nd;
-    const int cdim = nm > 0 ? cache_dim(h) : 0;
+    const int cdim = cache_dim(h);
     const size_t dim = head + od + cdim;   /* = reset_table_dim(h) */
     bioim_handle_t *tmp = nullptr;
     int rc = bioim_create(&h->pack, nr, h->device, h->precision, h->seed, &tmp);
