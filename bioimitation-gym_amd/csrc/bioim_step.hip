@@ -123,7 +123,12 @@ DEV void sfor(F &&f) {
 #define BIOIM_FV_PE_PLANAR 0
 #endif
 /* the reset table (LaunchArgs::reset_tab) in the planar RK-Merson step
- * kernels too (the spatial ones stay as they are: 506-512 registers) */
+ * kernels too, and (round 6) in the spatial ones: they fit it at 486-512
+ * registers with no scratch; same-box reference-integrator legs C4 +3.9 %,
+ * LockedKnee3D +4.4 %, Palsy3D +5.6 % (profiles/r06/r06e/ab_rk.txt) */
+#ifndef BIOIM_RESET_TAB_RK_SPATIAL
+#define BIOIM_RESET_TAB_RK_SPATIAL 1
+#endif
 #ifndef BIOIM_RESET_TAB_RK
 #define BIOIM_RESET_TAB_RK 1
 #endif
@@ -3513,7 +3518,7 @@ DEV void env_block(const LaunchArgs<T, Real> &a, int blk) {
             pending_reset = true;
             do_reset = true;
             reset_row = draw_index(a.seed, a.env_offset + env, resets, M.reset_hi);
-            if constexpr ((!RK || (BIOIM_RESET_TAB_RK && T::PLANAR)) && !PERT && !REP) {
+            if constexpr ((!RK || (BIOIM_RESET_TAB_RK && (T::PLANAR || BIOIM_RESET_TAB_RK_SPATIAL))) && !PERT && !REP) {
                 /* the reset table (LaunchArgs::reset_tab): the state the reset
                  * realize would leave (reference row, default activation,
                  * equilibrium fiber lengths) and its observation, without a
@@ -4135,7 +4140,7 @@ struct bioim_handle {
  * default kernels (no push table, semi-implicit) and no force report or
  * state storage (their rows come from the reset realize itself) */
 static inline bool reset_table_wanted(const bioim_handle_t *h) {
-    return h->reset_tab_on && h->auto_reset && h->pert_n == 0 && (!h->rk || (BIOIM_RESET_TAB_RK && h->planar)) &&
+    return h->reset_tab_on && h->auto_reset && h->pert_n == 0 && (!h->rk || (BIOIM_RESET_TAB_RK && (h->planar || BIOIM_RESET_TAB_RK_SPATIAL))) &&
            !h->force_out && !h->traj;
 }
 static inline bool reset_table_eligible(const bioim_handle_t *h) { return h->reset_tab && reset_table_wanted(h); }

@@ -921,7 +921,10 @@ def test_parity_200_steps_muscle_tracking_drive(env_id):
                                                # with its raw action) and the torque branch of the planar RK kernel
                                                ('MuscleRunningImitation3D-v0', 'semi-implicit'),
                                                ('MusclePalsyImitation3D-v0', 'semi-implicit'),
-                                               ('TorqueWalkingImitation2D-v0', 'rk-merson')])
+                                               ('TorqueWalkingImitation2D-v0', 'rk-merson'),
+                                               # round 6: the spatial RK kernels read the table too
+                                               ('MuscleRunningImitation3D-v0', 'rk-merson'),
+                                               ('MuscleLockedKneeImitation3D-v0', 'rk-merson')])
 def test_reset_table_matches_reset_realize(env_id, integrator):
     """In-kernel auto-resets from the reset table (bioim_set_reset_table, the
     default) against the reset realize run in the step launch (table off):
