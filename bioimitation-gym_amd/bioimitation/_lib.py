@@ -19,7 +19,7 @@ EXPORTS = ['bioim_create', 'bioim_destroy', 'bioim_reset', 'bioim_step', 'bioim_
            'bioim_get_state', 'bioim_set_state', 'bioim_query', 'bioim_query_launch', 'bioim_stream', 'bioim_set_stream', 'bioim_sync',
            'bioim_last_error', 'bioim_modelpack_size', 'bioim_build_id', 'bioim_reset_count', 'bioim_set_final_obs', 'bioim_set_integrator', 'bioim_force_report_dim', 'bioim_set_force_report',
            'bioim_set_rk_budget', 'bioim_pending_count', 'bioim_set_active_mask', 'bioim_osim', 'bioim_osim_report_dim', 'bioim_eval_count', 'bioim_set_state_storage',
-           'bioim_finished_count', 'bioim_set_rk_counters']
+           'bioim_finished_count', 'bioim_set_rk_counters', 'bioim_copy_state']
 
 _lib = None
 
@@ -75,6 +75,7 @@ def load():
         'bioim_eval_count': (C.c_int, [vp, C.POINTER(C.c_uint64)]),
         'bioim_finished_count': (C.c_int, [vp, C.POINTER(C.c_uint64)]),
         'bioim_set_rk_counters': (C.c_int, [vp, C.c_uint32, C.c_uint32]),
+        'bioim_copy_state': (C.c_int, [vp, vp]),
         'bioim_set_state_storage': (C.c_int, [vp, vp, C.c_int, vp]),
     }
     for name, (res, args) in sig.items():

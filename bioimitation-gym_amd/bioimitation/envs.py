@@ -111,8 +111,11 @@ class ImitationEnv:
         self._last = None            # (reward, all_rewards, done) of the last step
         self.state_dict = None
         self._record = bool(cfg.get('record_trajectory', True))
+        self._state_buf = None
         if self._record:
+            import torch
             self._env.enable_force_report()
+            self._state_buf = torch.empty((1, self._env.state_dim), dtype=torch.float64, device=self._env.device)
             if self._env.integrator == 'rk-merson':
                 self._env.enable_state_storage(512)    # the Manager's rows: every accepted step
         ntrans = sum(1 for c in (pk.coord_tx, pk.coord_ty, pk.coord_tz) if c >= 0)
@@ -128,13 +131,15 @@ class ImitationEnv:
             self._names = load_names(self.env_id)
         return obs_to_dict(o, self._env.pack, self._names)
 
-    def _record_row(self, o, stepped=True, fr=None):
-        """o: the env's observation row on the host; fr: its force-report row
-        when the caller has already copied it"""
+    def _record_row(self, o, stepped=True, fr=None, state=None):
+        """o: the env's observation row on the host; fr, state: its
+        force-report and state rows when the caller has already copied them"""
         if self._record:
             if fr is None:
                 fr = self._env.force_report[0].double().cpu().numpy()
-            self.osim_model.record_row(self._env.get_state()[0], o[self._qdd], fr, stepped)
+            if state is None:
+                state = self._env.get_state()[0]
+            self.osim_model.record_row(state, o[self._qdd], fr, stepped)
 
     def reset(self, obs_as_dict=False):
         index = 0 if self.test else random.randint(0, self._env.pack.reset_hi)
@@ -156,11 +161,21 @@ class ImitationEnv:
         # the force-report row included when recording
         parts = [obs[0], rew[:1], info[0], done[:1].to(obs.dtype)]
         if self._record:
+            # the force-report row and the state row (gathered on the device,
+            # bioim_copy_state) ride in the same transfer: no separate
+            # synchronizing bioim_get_state per step
             parts.append(self._env.force_report[0])
+            if obs.dtype == torch.float64:   # fp32 envs keep get_state (t and q stay doubles)
+                parts.append(self._env.state_rows(self._state_buf)[0])
         out = torch.cat(parts).double().cpu().numpy()
         nobs, ninf = obs.shape[1], info.shape[1]
         o = out[:nobs]
-        self._record_row(o, fr=out[nobs + 1 + ninf + 1:] if self._record else None)
+        if self._record:
+            nfr = self._env.force_report.shape[1]
+            f0 = nobs + 1 + ninf + 1
+            self._record_row(o, fr=out[f0:f0 + nfr], state=out[f0 + nfr:] if len(out) > f0 + nfr else None)
+        else:
+            self._record_row(o)
         inf = [float(v) for v in out[nobs + 1:nobs + 1 + ninf]]
         self._last = (float(out[nobs]), inf, bool(out[nobs + 1 + ninf]))
         return [self._out(o[None, :], obs_as_dict), self._last[0], self._last[2], {'all_rewards': inf}]

@@ -311,6 +311,18 @@ class VectorEnv:
         _lib.check(self._L.bioim_get_state(self._h, s.ctypes.data_as(C.POINTER(C.c_double))))
         return s
 
+    def state_rows(self, out=None):
+        """The flat state rows of get_state as a (N, state_dim) float64 device
+        tensor, gathered on the env's stream without synchronizing
+        (bioim_copy_state): one transfer can carry them with a step's
+        outputs."""
+        import torch
+        if out is None:
+            out = torch.empty((self.num_envs, self.state_dim), dtype=torch.float64, device=self.device)
+        self._bind_stream()
+        _lib.check(self._L.bioim_copy_state(self._h, self._ptr(out)))
+        return out
+
     def set_state(self, s: np.ndarray):
         s = np.ascontiguousarray(s, dtype=np.float64)
         assert s.shape == (self.num_envs, self.state_dim)

@@ -4926,6 +4926,51 @@ int bioim_get_state(bioim_handle_t *h, double *host_state) {
     return h->precision == 64 ? xfer_state<double>(h, host_state, nullptr) : xfer_state<float>(h, host_state, nullptr);
 }
 
+/* bioim_copy_state: the flat state rows (bioim_get_state's layout) gathered
+ * on the device, one thread per value, on the handle's stream — no
+ * synchronization, so a caller can fold them into the copy of a step's
+ * outputs (the single-env recorder, envs.py) */
+extern "C++" {
+template <typename Real>
+__global__ void state_rows_kernel(DState<Real> st, int n, int nd, int nm, int na, int H, int dim, double *out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)n * dim) return;
+    const int e = (int)(i / dim);
+    int k = (int)(i % dim);
+    const size_t N = (size_t)n;
+    double v = 0;
+    if (k < 5) {
+        v = k == 0 ? st.t[e] : k == 1 ? (double)st.istep[e] : k == 2 ? (double)st.has_last[e]
+          : k == 3 ? (double)st.old_px[e] : (double)st.done[e];
+    } else if ((k -= 5) < nd) v = st.q[k * N + e];
+    else if ((k -= nd) < nd) v = st.u[k * N + e];
+    else if ((k -= nd) < nm) v = st.act[k * N + e];
+    else if ((k -= nm) < nm) v = st.lce[k * N + e];
+    else if ((k -= nm) < H * na) v = st.hist[k * N + e];   /* [hh][a] = hh * na + a */
+    else if ((k -= H * na) < na) v = st.last[k * N + e];
+    else if ((k -= na) == 0) v = st.hrk[e];
+    else v = st.ctl[(k - 1) * N + e];
+    out[i] = v;
+}
+}  // extern "C++"
+
+int bioim_copy_state(bioim_handle_t *h, void *device_out) {
+    if (!h || !device_out) return fail(BIOIM_E_ARG, "bioim_copy_state: bad arguments");
+    HIPCHK(hipSetDevice(h->device));
+    const int dim = bioim_state_dim(h), n = h->n;
+    const size_t total = (size_t)n * dim;
+    const int bs = 256;
+    const dim3 g((unsigned)((total + bs - 1) / bs)), b(bs);
+    if (h->precision == 64)
+        hipLaunchKernelGGL(state_rows_kernel<double>, g, b, 0, h->stream, *reinterpret_cast<DState<double> *>(h->dstate), n,
+                           h->ndof, h->nmuscle, h->nact, h->horizon, dim, reinterpret_cast<double *>(device_out));
+    else
+        hipLaunchKernelGGL(state_rows_kernel<float>, g, b, 0, h->stream, *reinterpret_cast<DState<float> *>(h->dstate), n,
+                           h->ndof, h->nmuscle, h->nact, h->horizon, dim, reinterpret_cast<double *>(device_out));
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 int bioim_set_state(bioim_handle_t *h, const double *host_state) {
     if (!h || !host_state) return fail(BIOIM_E_ARG, "bioim_set_state: bad arguments");
     HIPCHK(hipSetDevice(h->device));

@@ -84,7 +84,7 @@ int bioim_reset(bioim_handle_t *h, const int32_t *env_ids, const int32_t *ref_in
 int bioim_step(bioim_handle_t *h, const void *actions, void *obs, void *reward, uint8_t *done, void *info);
 int bioim_set_auto_reset(bioim_handle_t *h, int on);
 /* In-kernel auto-resets (default step kernels: no push table, semi-implicit
- * or planar RK-Merson, no force report / state storage) read the reset state
+ * or RK-Merson, no force report / state storage) read the reset state
  * and observation of the drawn reference row from a per-handle table (torque
  * models: with M^-1 at the row, for the held torques' share of q'')
  * instead of running the reset realize with fiber equilibrium in the step
@@ -92,8 +92,9 @@ int bioim_set_auto_reset(bioim_handle_t *h, int on);
  * table is built once, on the first such step, by that same reset realize
  * (one scratch env per reference row); that step blocks while it is built
  * (milliseconds).  on = 1 (default) uses it, 0 runs the
- * realize in the launch as before; results agree to the rounding level of
- * the fiber-velocity root (its warm start differs).  Replaces nothing in the
+ * realize in the launch as before, with the same results bit for bit (both
+ * start the fiber-velocity roots cold; the row also carries the reset
+ * realize's cache for the next step's first substep).  Replaces nothing in the
  * reference (OsimModel.reset + equilibrateMuscles per reset,
  * opensim_wrapper.py:293-297). */
 int bioim_set_reset_table(bioim_handle_t *h, int on);
@@ -205,6 +206,13 @@ int bioim_set_env_offset(bioim_handle_t *h, int offset);
 int bioim_state_dim(const bioim_handle_t *h);
 int bioim_get_state(bioim_handle_t *h, double *host_state /* [N][state_dim] */);
 int bioim_set_state(bioim_handle_t *h, const double *host_state);
+/* The same rows as bioim_get_state, written as doubles into a device buffer
+ * [N][state_dim] on the handle's stream, without synchronizing (the
+ * single-env recorder copies them with the step's outputs in one transfer).
+ * Rows of envs suspended mid-step by the RK budget are not at a step
+ * boundary (bioim_get_state refuses them; this call does not check).  No
+ * reference counterpart. */
+int bioim_copy_state(bioim_handle_t *h, void *device_out);
 
 /* Integrator of the physics between env steps.  kind 0: the fixed
  * semi-implicit substeps (the pack's nsub; default).  kind 1: the reference's

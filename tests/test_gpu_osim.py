@@ -478,3 +478,23 @@ def test_state_storage_overflow_grows_buffer(tmp_path):
     with pytest.warns(RuntimeWarning, match=f'{lost} accepted integration steps'):
         om.save_simulation(str(tmp_path))
     env.close()
+
+
+@pytest.mark.parametrize('env_id,precision', [('MuscleWalkingImitation2D-v0', 64), ('TorqueWalkingImitation3D-v0', 32),
+                                              ('MuscleRunningImitation3D-v0', 64)])
+def test_copy_state_rows_equal_get_state(env_id, precision):
+    """bioim_copy_state (the single-env recorder's state row, gathered on the
+    device and copied with the step's outputs) gives get_state's rows, bit
+    for bit, after resets and steps with auto-resets"""
+    import torch
+    from bioimitation.vector_env import VectorEnv
+    env = VectorEnv(env_id, 40, precision=precision, seed=3, auto_reset=True)
+    env.reset()
+    g = torch.Generator(device='cuda').manual_seed(1)
+    for t in range(30):
+        a = torch.rand((env.num_envs, env.action_dim), generator=g, device=env.device, dtype=env.dtype)
+        env.step(a)
+        if t % 10 == 9:
+            rows = env.state_rows().cpu().numpy()
+            np.testing.assert_array_equal(rows, env.get_state())
+    env.close()
