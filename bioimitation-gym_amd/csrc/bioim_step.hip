@@ -772,6 +772,11 @@ template <class T, typename Real> struct Lay {
 #ifndef BIOIM_REALIZE_CACHE_TORQUE
 #define BIOIM_REALIZE_CACHE_TORQUE 1
 #endif
+/* the spatial kernels load the cache row at the substep (0) or at kernel
+ * start like the planar ones (1) */
+#ifndef BIOIM_CACHE_PREFETCH_SPATIAL
+#define BIOIM_CACHE_PREFETCH_SPATIAL 0
+#endif
 template <class T> struct CacheLay {
     /* torque models: the cached right-hand side leaves out the actuator
      * torques (the controls), which the cached substep adds */
@@ -779,7 +784,7 @@ template <class T> struct CacheLay {
                                (T::NM > 0 ? (T::PLANAR || BIOIM_REALIZE_CACHE_SPATIAL) : BIOIM_REALIZE_CACHE_TORQUE);
     /* planar kernels load the row at kernel start, ahead of the action
      * pre-processing; the spatial ones (no register headroom) at the substep */
-    static constexpr bool PREFETCH = T::PLANAR;
+    static constexpr bool PREFETCH = T::PLANAR || BIOIM_CACHE_PREFETCH_SPATIAL;
     static constexpr int ND = T::ND > 0 ? T::ND : 1, NP = ND * (ND + 1) / 2;
     static constexpr int SYS = NP + ND;          /* [NP] packed lower M(h), [ND] rhs(h): LDS MP..RHS order */
     static constexpr int MUS = SYS;              /* [NM][3] fiber-velocity root, dv/dl, clamped (0 / 1) */
