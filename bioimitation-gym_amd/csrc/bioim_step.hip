@@ -1818,8 +1818,9 @@ DEV Real pert_force(const PertArgs<Real> &P, double *sl, int k) {
  * CACHE kernels (CacheLay): CI.make — a realize also forms the implicit
  * system at h = CI.hc and stores it with the fiber-velocity roots into the
  * env's cache row (CI.row()); CI.use — a first substep takes its system and
- * roots from the cache (CI.sys / CI.mus, loaded at kernel start) and only
- * solves: the state is the one the last realize ran at. */
+ * roots from the cache (CI.sys / CI.mus loaded at kernel start in the
+ * planar kernels, the row itself in the spatial ones) and only solves: the
+ * state is the one the last realize ran at. */
 template <class T, typename Real> struct CacheIO {
     static constexpr int PF = CacheLay<T>::PF > 0 ? CacheLay<T>::PF : 1;
     static constexpr int PFA = CacheLay<T>::PREFETCH ? PF : 1, MPA = CacheLay<T>::PREFETCH ? Lay<T, Real>::MPL : 1;
@@ -1847,7 +1848,7 @@ DEV void dynamics(const DModel<Real> &M, const SModel<T, Real> &SM, Real qd, Rea
                   const PertArgs<Real> &P, double *pslot, int pk, Dyn<T, Real> &D, const CacheIO<T, Real> &CI) {
     using LY = Lay<T, Real>;
     constexpr int ND = LY::ND, NP = LY::NP, NB = T::NB, G = T::G, MPL = LY::MPL;
-    static_assert(!CACHE || (CacheLay<T>::ON && IMP && !PERT), "the realize cache: semi-implicit planar muscle kernels");
+    static_assert(!CACHE || (CacheLay<T>::ON && IMP && !PERT), "the realize cache: the default (semi-implicit, no push) step kernels");
     static_assert(NB < G && ND <= G, "lane NB writes the ground slot; one lane per dof");
     /* the semi-implicit planar kernels: the implicit contact / limit terms
      * without a branch on h (the spatial kernels keep it: register budget) */
@@ -4982,24 +4983,27 @@ int bioim_set_state(bioim_handle_t *h, const double *host_state) {
     return h->precision == 64 ? xfer_state<double>(h, nullptr, host_state) : xfer_state<float>(h, nullptr, host_state);
 }
 
+/* one per-env plane of the device state (a DState member; the pointer
+ * layout is the same for both precisions), copied to the host — the
+ * counters read that plane alone, not the whole state (round 6: with the
+ * realize cache the state is ~10 MB at 4096 envs) */
+extern "C++" template <typename V> static int read_plane(bioim_handle_t *h, V *DState<double>::*member, std::vector<V> &out) {
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipStreamSynchronize(h->side));
+    const DState<double> &st = *reinterpret_cast<const DState<double> *>(h->dstate);
+    out.resize((size_t)h->n);
+    HIPCHK(hipMemcpy(out.data(), st.*member, sizeof(V) * (size_t)h->n, hipMemcpyDeviceToHost));
+    return 0;
+}
+
 /* total resets (explicit + in-kernel auto-resets) over the handle's envs */
 int bioim_reset_count(bioim_handle_t *h, uint64_t *total) {
     if (!h || !total) return fail(BIOIM_E_ARG, "bioim_reset_count: bad arguments");
-    HIPCHK(hipSetDevice(h->device));
-    std::vector<char> buf(h->state_bytes);
-    HIPCHK(hipStreamSynchronize(h->stream));
-    HIPCHK(hipStreamSynchronize(h->side));
-    HIPCHK(hipMemcpy(buf.data(), h->state_buf, h->state_bytes, hipMemcpyDeviceToHost));
+    std::vector<int32_t> r;
+    if (const int rc = read_plane<int32_t>(h, &DState<double>::resets, r)) return rc;
     uint64_t sum = 0;
-    if (h->precision == 64) {
-        DState<double> hs;
-        state_layout<double>(h, buf.data(), &hs);
-        for (int e = 0; e < h->n; ++e) sum += (uint32_t)hs.resets[e];
-    } else {
-        DState<float> hs;
-        state_layout<float>(h, buf.data(), &hs);
-        for (int e = 0; e < h->n; ++e) sum += (uint32_t)hs.resets[e];
-    }
+    for (int e = 0; e < h->n; ++e) sum += (uint32_t)r[e];
     *total = sum;
     return 0;
 }
@@ -5007,21 +5011,10 @@ int bioim_reset_count(bioim_handle_t *h, uint64_t *total) {
 /* one of the per-env RK counters of the state (DState::rkev) summed over the envs */
 static int rk_counter(bioim_handle_t *h, uint64_t *total, bool fin, const char *who) {
     if (!h || !total) return fail(BIOIM_E_ARG, std::string(who) + ": bad arguments");
-    HIPCHK(hipSetDevice(h->device));
-    std::vector<char> buf(h->state_bytes);
-    HIPCHK(hipStreamSynchronize(h->stream));
-    HIPCHK(hipStreamSynchronize(h->side));
-    HIPCHK(hipMemcpy(buf.data(), h->state_buf, h->state_bytes, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> r;
+    if (const int rc = read_plane<uint64_t>(h, &DState<double>::rkev, r)) return rc;
     uint64_t sum = 0;
-    if (h->precision == 64) {
-        DState<double> hs;
-        state_layout<double>(h, buf.data(), &hs);
-        for (int e = 0; e < h->n; ++e) sum += (uint32_t)(fin ? hs.rkev[e] >> 32 : hs.rkev[e]);
-    } else {
-        DState<float> hs;
-        state_layout<float>(h, buf.data(), &hs);
-        for (int e = 0; e < h->n; ++e) sum += (uint32_t)(fin ? hs.rkev[e] >> 32 : hs.rkev[e]);
-    }
+    for (int e = 0; e < h->n; ++e) sum += (uint32_t)(fin ? r[e] >> 32 : r[e]);
     *total = sum;
     return 0;
 }

@@ -1084,3 +1084,60 @@ def test_c4_auto_reset_rows_vs_oracle_reset():
     assert checked >= 100 and len(drawn) >= 30, (checked, len(drawn))
     assert worst_obs < 1e-9 and worst_lce < 1e-9, (worst_obs, worst_lce)
     env.close()
+
+
+@pytest.mark.skipif(not gpu_available(), reason='needs GPU')
+@pytest.mark.parametrize('env_id', ['MuscleWalkingImitation2D-v0', 'TorqueWalkingImitation2D-v0',
+                                    'MuscleRunningImitation3D-v0', 'TorqueWalkingImitation3D-v0'])
+def test_realize_cache_first_substep(env_id):
+    """The realize cache: a launch's first substep solves the
+    implicit system the previous realize formed.  Against the same steps with
+    the cache invalidated before every launch (bioim_set_state clears it, so
+    every first substep runs the whole dynamics call): torque models give the
+    same bits (the realize formed that system with the substep's own
+    arithmetic at the substep's h; the actuator torques are added the same
+    way); muscle models agree to the rounding level and differ somewhere (the
+    first substep's fiber-velocity roots are the realize's warm-started ones
+    instead of a cold start: the cached path really ran).  The cached run
+    stays within the usual bound of the oracle."""
+    import torch
+    from bioimitation.vector_env import VectorEnv
+    import oracle
+    from bioimitation.registry import load_pack
+    n, T = 64, 25
+    pk = load_pack(env_id)
+    rows = np.random.default_rng(4).integers(0, pk.reset_hi + 1, size=n)
+    a = VectorEnv(env_id, n, precision=64, seed=2)
+    b = VectorEnv(env_id, n, precision=64, seed=2)
+    a.reset(ref_index=rows)
+    b.reset(ref_index=rows)
+    orc = oracle.Oracle(pk)
+    bufs = orc.new_envs(n)
+    for i in range(n):
+        orc.reset(bufs, i, int(rows[i]))
+    rng = np.random.default_rng(5)
+    worst_ab, worst_orc, differs = 0.0, 0.0, False
+    for t in range(T):
+        if pk.nmuscle:
+            act = rng.uniform(0.0, 1.0, size=(n, pk.nact))
+        else:
+            act = np.array([[pk.ref_q[min(int(r) + t + 1, pk.nrows - 1)][pk.pd_coord[i]] for i in range(pk.nact)]
+                            for r in rows]) + rng.normal(0.0, 0.05, size=(n, pk.nact))
+        oa = a.step(torch.as_tensor(act, device=a.device))[0].cpu().numpy()
+        b.set_state(b.get_state())          # invalidates b's cache rows
+        ob = b.step(torch.as_tensor(act, device=b.device))[0].cpu().numpy()
+        d = _rel(oa, ob)
+        worst_ab = max(worst_ab, float(d.max()))
+        differs = differs or bool((oa != ob).any())
+        for i in range(n):
+            o, _, _, _ = orc.step(bufs, i, act[i])
+            worst_orc = max(worst_orc, float(_rel(oa[i], o).max()))
+    print(f'{env_id}: cached vs uncached first substep max rel diff {worst_ab:.1e}; cached vs oracle {worst_orc:.1e}')
+    if pk.nmuscle:
+        assert differs, 'the cached first substep never ran (results bit-equal to the uncached run)'
+        assert worst_ab < 1e-9, worst_ab
+    else:
+        assert not differs, worst_ab
+    assert worst_orc < 1e-6, worst_orc
+    a.close()
+    b.close()
