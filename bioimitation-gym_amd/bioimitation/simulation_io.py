@@ -61,9 +61,34 @@ class TrajectoryRecorder:
         self.clear()
 
     def clear(self):
-        self.rows = []
-        self.force_rows = []
-        self.state_rows = []
+        self._rows = []
+        self._force_rows = []
+        self._state_rows = []
+        self._pending = []
+
+    # rows are formed when read: record() keeps copies of its arguments, so an
+    # env step pays for three small copies instead of the row assembly
+    # (the single-env facade records every step)
+    @property
+    def rows(self):
+        self._flush()
+        return self._rows
+
+    @property
+    def force_rows(self):
+        self._flush()
+        return self._force_rows
+
+    @property
+    def state_rows(self):
+        self._flush()
+        return self._state_rows
+
+    def _flush(self):
+        if self._pending:
+            pending, self._pending = self._pending, []
+            for args in pending:
+                self._record_now(*args)
 
     def _full(self, t, qd, ud, act, lce):
         free = self.dof >= 0
@@ -80,8 +105,16 @@ class TrajectoryRecorder:
         integration steps (bioim_set_state_storage rows: t, q, u, activation,
         fiber length in dof order) — the States storage rows of the step
         (default: the step's end state)."""
+        if storage is None:
+            self._pending.append((np.array(state_row, dtype=np.float64), np.array(qdd, dtype=np.float64),
+                                  None if forces is None else np.array(forces, dtype=np.float64)))
+            return
+        self._flush()
+        self._record_now(state_row, qdd, forces, storage)
+
+    def _record_now(self, state_row, qdd, forces=None, storage=None):
         if forces is not None:
-            self.force_rows.append(np.concatenate([[float(state_row[0])], np.asarray(forces, dtype=np.float64)]))
+            self._force_rows.append(np.concatenate([[float(state_row[0])], np.asarray(forces, dtype=np.float64)]))
         pk = self.pack
         nd, nm = pk.ndof, pk.nmuscle
         t = float(state_row[0])
@@ -91,12 +124,12 @@ class TrajectoryRecorder:
         lce = state_row[5 + 2 * nd + nm:5 + 2 * nd + 2 * nm]
         full = self._full(t, qd, ud, act, lce)
         nc = self.nc
-        self.rows.append(np.concatenate([full[:1 + 2 * nc], np.asarray(qdd, dtype=np.float64), full[1 + 2 * nc:]]))
+        self._rows.append(np.concatenate([full[:1 + 2 * nc], np.asarray(qdd, dtype=np.float64), full[1 + 2 * nc:]]))
         if storage is None:
-            self.state_rows.append(full)
+            self._state_rows.append(full)
         else:
             for r in np.asarray(storage, dtype=np.float64):
-                self.state_rows.append(self._full(r[0], r[1:1 + nd], r[1 + nd:1 + 2 * nd], r[1 + 2 * nd:1 + 2 * nd + nm],
+                self._state_rows.append(self._full(r[0], r[1:1 + nd], r[1 + nd:1 + 2 * nd], r[1 + 2 * nd:1 + 2 * nd + nm],
                                                   r[1 + 2 * nd + nm:1 + 2 * nd + 2 * nm]))
 
     def record_steps(self, state_rows, qdd_rows, force_rows):

@@ -150,11 +150,25 @@ class VectorEnv:
             self.final_obs = None
         _lib.check(self._L.bioim_set_final_obs(self._h, self._ptr(self.final_obs)))
 
-    def enable_force_report(self, on: bool = True):
+    @property
+    def force_report_dim(self) -> int:
+        """F of the force-report rows (bioim_force_report_dim)"""
+        return _lib.check(self._L.bioim_force_report_dim(self._h))
+
+    def enable_force_report(self, on: bool = True, out=None):
         """Per-force-element values of every realized state in
-        ``self.force_report`` (N, F), F = bioim_force_report_dim (include/bioim.h)."""
+        ``self.force_report`` (N, F), F = bioim_force_report_dim (include/bioim.h);
+        ``out``: a contiguous (N, F) tensor of the env's dtype and device to
+        write them to instead (e.g. a view of a larger buffer)."""
         import torch
-        if on and getattr(self, 'force_report', None) is None:
+        if on and out is not None:
+            f = self.force_report_dim
+            if out.shape != (self.num_envs, f) or out.dtype != self.dtype or out.device != self.device \
+                    or not out.is_contiguous():
+                raise ValueError(f'force report buffer must be a contiguous ({self.num_envs}, {f}) {self.dtype} '
+                                 f'tensor on {self.device}')
+            self.force_report = out
+        elif on and getattr(self, 'force_report', None) is None:
             f = _lib.check(self._L.bioim_force_report_dim(self._h))
             self.force_report = torch.zeros((self.num_envs, f), dtype=self.dtype, device=self.device)
         elif not on:
