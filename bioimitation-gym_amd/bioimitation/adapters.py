@@ -121,6 +121,17 @@ class RLlibVectorEnv:
                              auto_reset=False, env_offset=env_offset)
         self.num_envs = num_envs
         self.observation_space, self.action_space = _spaces(self.env)
+        # pinned host mirrors: the actions go up, and reward, done and info
+        # come back, in asynchronous copies on the env's stream; the
+        # observation's blocking copy then waits for all of them (one wait
+        # per step instead of four)
+        import torch
+        e, dt = self.env, self.env.dtype
+        pin = dict(dtype=dt, pin_memory=True)
+        self._act = (torch.zeros((num_envs, e.action_dim), dtype=dt, device=e.device),
+                     torch.zeros((num_envs, e.action_dim), **pin))
+        self._host = (torch.zeros(num_envs, **pin), torch.zeros(num_envs, dtype=torch.uint8, pin_memory=True),
+                      torch.zeros((num_envs, e.info_dim), **pin))
 
     def vector_reset(self):
         return list(self.env.reset().double().cpu().numpy())
@@ -131,9 +142,21 @@ class RLlibVectorEnv:
 
     def vector_step(self, actions):
         import torch
-        a = torch.as_tensor(np.asarray(actions, dtype=np.float64), device=self.env.device)
-        obs, rew, done, info = self.env.step(a)
-        obs, rew, done, info = (t.double().cpu().numpy() for t in (obs, rew, done, info))
+        e = self.env
+        a = np.asarray(actions, dtype=np.float64)
+        if a.shape != (self.num_envs, e.action_dim):
+            raise ValueError(f'actions must be ({self.num_envs}, {e.action_dim}), got {a.shape}')
+        a_dev, a_pin = self._act
+        # the last step's copies finished at its synchronize: the pinned buffers are free
+        a_pin.numpy()[:] = a
+        a_dev.copy_(a_pin, non_blocking=True)
+        obs, rew, done, info = e.step(a_dev)
+        for h, d in zip(self._host, (rew, done, info)):
+            h.copy_(d, non_blocking=True)
+        obs = obs.double().cpu().numpy()     # blocking, on the same stream: behind the copies above
+        # fresh arrays: RLlib may keep the rows past the next step
+        rew, done, info = (h.numpy().astype(np.float64) if h.dtype != torch.uint8 else h.numpy().copy()
+                           for h in self._host)
         infos = [{'all_rewards': list(map(float, r))} for r in info]
         return list(obs), list(map(float, rew)), list(map(bool, done)), infos
 

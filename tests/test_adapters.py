@@ -62,12 +62,19 @@ def test_rllib_vector_env_protocol():
     assert len(obs) == n and obs[0].shape == (138,) and venv.action_space.shape == (14,)
     np.testing.assert_array_equal(np.stack(obs), ref.reset().cpu().numpy())
     rng = np.random.default_rng(0)
+    kept = None
     for t in range(5):
         a = rng.uniform(0, 1, (n, 14))
         o, r, d, i = venv.vector_step(list(a))
         ro, rr, rd, ri = ref.step(torch.as_tensor(a, device=ref.device))
         np.testing.assert_array_equal(np.stack(o), ro.cpu().numpy())
         assert r == list(map(float, rr.cpu().numpy())) and len(i[0]['all_rewards']) == 5
+        assert d == list(map(bool, rd.cpu().numpy()))
+        # the rows a step returned are the caller's: the next step (through
+        # the same pinned buffers) leaves them alone
+        if kept is not None:
+            np.testing.assert_array_equal(np.stack(kept[0]), kept[1])
+        kept = (o, np.stack(o).copy())
     o3 = venv.reset_at(3)
     assert o3.shape == (138,) and np.isfinite(o3).all()
     venv.close()
