@@ -241,10 +241,20 @@ class RLlibBaseEnv:
         self._fresh = np.zeros(num_envs, dtype=bool)      # results not yet polled
         self._from_reset = np.zeros(num_envs, dtype=bool)
         self._started = False
+        # poll(): reward, done and info come back in asynchronous copies into
+        # pinned buffers, the observation's blocking copy waits for them
+        pin = dict(dtype=self.env.dtype, pin_memory=True)
+        self._host = (torch.zeros(num_envs, **pin), torch.zeros(num_envs, dtype=torch.uint8, pin_memory=True),
+                      torch.zeros((num_envs, self.env.info_dim), **pin))
 
-    def _rows(self, t, ids):
-        import torch
-        return t[torch.as_tensor(ids, device=self.env.device)].double().cpu().numpy()
+    def _outputs(self, ids):
+        """host rows ``ids`` of obs, reward, done and info (fresh arrays)"""
+        e = self.env
+        for h, d in zip(self._host, (e.reward, e.done, e.info)):
+            h.copy_(d, non_blocking=True)
+        o = e.obs.double().cpu().numpy()     # blocking, on the same stream: behind the copies above
+        r, d, f = (h.numpy()[ids].astype(np.float64) for h in self._host)
+        return o[ids], r, d, f
 
     def poll(self):
         if not self._started:
@@ -256,7 +266,7 @@ class RLlibBaseEnv:
         A = self.AGENT
         obs, rew, done, info = {}, {}, {}, {}
         if len(ids):
-            o, r, d, f = (self._rows(t, ids) for t in (self.env.obs, self.env.reward, self.env.done, self.env.info))
+            o, r, d, f = self._outputs(ids)
             for k, i in enumerate(ids):
                 i = int(i)
                 obs[i] = {A: o[k]}
