@@ -498,3 +498,46 @@ def test_copy_state_rows_equal_get_state(env_id, precision):
             rows = env.state_rows().cpu().numpy()
             np.testing.assert_array_equal(rows, env.get_state())
     env.close()
+
+
+@pytest.mark.parametrize('env_id,record', [('TorqueWalkingImitation2D-v0', True), ('MuscleWalkingImitation2D-v0', True),
+                                           ('TorqueWalkingImitation2D-v0', False)])
+def test_facade_packed_step_matches_vector_env(env_id, record):
+    """The single-env facade's step (envs.py _bind_packed: one packed output
+    buffer with the done byte inside it, pinned action and output copies)
+    returns what a plain one-env VectorEnv gives for the same actions, bit for
+    bit, through terminations and resets; the recorder holds one row per
+    step since the last reset, the last at the env's state"""
+    import torch
+    from bioimitation import envs
+    from bioimitation.vector_env import VectorEnv
+    f = envs.make(env_id, config={'mode': 'test', 'record_trajectory': record})
+    v = VectorEnv(env_id, 1, config=dict(f.config, apply_perturbations=False), seed=0, auto_reset=False)
+    pk = v.pack
+    rng = np.random.default_rng(5)
+    f.reset()
+    v.reset(env_ids=[0], ref_index=[0])
+    since_reset, dones = 0, 0
+    for t in range(300):    # random actions: the model falls, so episodes end (asserted below)
+        if pk.nmuscle:
+            a = rng.uniform(0.0, 1.0, size=pk.nact)
+        else:
+            a = rng.uniform(-1.0, 1.0, size=pk.nact)
+        o, r, d, info = f.step(a)
+        vo, vr, vd, vi = v.step(torch.as_tensor(a[None, :], device=v.device))
+        np.testing.assert_array_equal(o, vo[0].cpu().numpy())
+        assert r == float(vr[0]) and d == bool(vd[0]) and info['all_rewards'] == [float(x) for x in vi[0]]
+        since_reset += 1
+        if record:
+            rec = f.osim_model.recorder
+            assert len(rec.rows) == since_reset + 1                 # the reset row, then one per step
+            assert rec.state_rows[-1][0] == v.get_state()[0][0]    # the last row's time: the env's
+        if d:
+            dones += 1
+            f.reset()
+            v.reset(env_ids=[0], ref_index=[0])
+            since_reset = 0
+    np.testing.assert_array_equal(f._env.get_state(), v.get_state())
+    assert dones > 0
+    f.close()
+    v.close()
