@@ -500,19 +500,24 @@ def test_copy_state_rows_equal_get_state(env_id, precision):
     env.close()
 
 
-@pytest.mark.parametrize('env_id,record', [('TorqueWalkingImitation2D-v0', True), ('MuscleWalkingImitation2D-v0', True),
-                                           ('TorqueWalkingImitation2D-v0', False)])
-def test_facade_packed_step_matches_vector_env(env_id, record):
-    """The single-env facade's step (envs.py _bind_packed: one packed output
-    buffer with the done byte inside it, pinned action and output copies)
-    returns what a plain one-env VectorEnv gives for the same actions, bit for
-    bit, through terminations and resets; the recorder holds one row per
-    step since the last reset, the last at the env's state"""
+@pytest.mark.parametrize('env_id,record,precision', [('TorqueWalkingImitation2D-v0', True, 64),
+                                                     ('MuscleWalkingImitation2D-v0', True, 64),
+                                                     ('TorqueWalkingImitation2D-v0', False, 64),
+                                                     ('MuscleWalkingImitation2D-v0', True, 32)])
+def test_facade_packed_step_matches_vector_env(env_id, record, precision):
+    """The single-env facade's step (fp64, envs.py _bind_packed: one packed
+    output buffer with the done byte inside it, pinned action and output
+    copies; fp32: the concatenating path) returns what a plain one-env
+    VectorEnv gives for the same actions, bit for bit, through terminations
+    and resets; the recorder holds one row per step since the last reset,
+    the last at the env's state"""
     import torch
     from bioimitation import envs
     from bioimitation.vector_env import VectorEnv
-    f = envs.make(env_id, config={'mode': 'test', 'record_trajectory': record})
-    v = VectorEnv(env_id, 1, config=dict(f.config, apply_perturbations=False), seed=0, auto_reset=False)
+    f = envs.make(env_id, config={'mode': 'test', 'record_trajectory': record}, precision=precision)
+    assert (f._packed is not None) == (precision == 64)
+    v = VectorEnv(env_id, 1, config=dict(f.config, apply_perturbations=False), seed=0, auto_reset=False,
+                  precision=precision)
     pk = v.pack
     rng = np.random.default_rng(5)
     f.reset()
@@ -524,8 +529,8 @@ def test_facade_packed_step_matches_vector_env(env_id, record):
         else:
             a = rng.uniform(-1.0, 1.0, size=pk.nact)
         o, r, d, info = f.step(a)
-        vo, vr, vd, vi = v.step(torch.as_tensor(a[None, :], device=v.device))
-        np.testing.assert_array_equal(o, vo[0].cpu().numpy())
+        vo, vr, vd, vi = v.step(torch.as_tensor(a[None, :], device=v.device, dtype=v.dtype))
+        np.testing.assert_array_equal(o, vo[0].double().cpu().numpy())
         assert r == float(vr[0]) and d == bool(vd[0]) and info['all_rewards'] == [float(x) for x in vi[0]]
         since_reset += 1
         if record:
